@@ -1,0 +1,136 @@
+/*
+ * nanopow.h -- C ABI of libnanopow.so, the MI355X (gfx950) Nano proof-of-work engine.
+ *
+ * This library replaces the compute core of the reference's work server,
+ * client/bin/windows/nano-work-server.exe (Rust + OpenCL; source not vendored,
+ * upstream nanocurrency/nano-work-server v1.0).  The DPoW client never calls
+ * this ABI directly: client/work_handler.py:53,75-78,104-108 talks HTTP JSON
+ * to a work server, and this repository's work server
+ * (nano-dpow_amd/nanopow/server.py) binds these symbols through ctypes.
+ *
+ * Conventions
+ *   - Every function is exception-free and returns int status unless noted:
+ *       NPOW_OK (0) found / done, NPOW_CANCELLED (1), NPOW_EXHAUSTED (2),
+ *       negative = error; npow_last_error() then returns a thread-local message.
+ *   - A root (block hash) is 32 raw bytes in the order of its hex string.
+ *   - Nonces, thresholds and work values are host-endian uint64_t.  The work
+ *     string a client sees is the big-endian hex of the nonce ("%016llx"),
+ *     while the bytes hashed are the nonce little-endian (dpow_server.py:130).
+ *   - work value = LE_u64(BLAKE2b-64(LE64(nonce) || root)); work is valid iff
+ *     value >= threshold (nano-work-server.exe @1661643 `nano_work`:
+ *     `if (blake2b(attempt_l, item_a) >= difficulty)`).
+ *   - Buffers are caller-owned; the library keeps no pointer past a call
+ *     (the `cancel` word is read only while the call runs).
+ *   - device_mask bit d selects HIP device d; 0 means "all devices".
+ *   - Calls that use disjoint device sets may run concurrently from
+ *     different threads; calls that share a device serialise on it.
+ */
+#ifndef NANOPOW_H
+#define NANOPOW_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NPOW_OK 0
+#define NPOW_CANCELLED 1
+#define NPOW_EXHAUSTED 2
+#define NPOW_ERR_NOT_INITIALISED (-1)
+#define NPOW_ERR_NO_DEVICE (-2)
+#define NPOW_ERR_BAD_ARGUMENT (-3)
+#define NPOW_ERR_HIP (-4)
+#define NPOW_ERR_INVALID_WORK (-5) /* GPU result failed CPU re-validation 3 times in a row */
+#define NPOW_ERR_CAPACITY (-6)     /* sweep found more hits than `cap` (n_out still exact) */
+
+/* Per-device counters; kernel_ms is measured with HIP events recorded on the
+ * stream each kernel is launched on (bench.py's roofline leg reads these). */
+typedef struct npow_device_stats {
+  uint64_t launches;      /* kernel launches (search + sweep + values) */
+  uint64_t nonces;        /* nonces whose hash the kernels computed */
+  double kernel_ms;       /* sum of per-launch event-timed durations */
+  uint64_t invalid_work;  /* GPU winners rejected by CPU re-validation */
+  int32_t cus;            /* compute units */
+  int32_t grid;           /* workgroups per search/sweep launch */
+} npow_device_stats;
+
+/* Open every visible HIP device, create its stream and buffers.
+ * Replaces the work server's OpenCL device set-up for `--gpu P:D[:THREADS]`
+ * (nano-work-server.exe @1681064).  Idempotent. */
+int npow_init(int* n_devices);
+
+/* Release every device resource.  Safe to call more than once. */
+void npow_shutdown(void);
+
+/* Thread-local description of the last error on this thread ("" if none). */
+const char* npow_last_error(void);
+
+/* CPU work value of one (root, nonce): the CPU re-validation the work server
+ * applies to every GPU result ("GPU returned invalid work", nano-work-server.exe
+ * @1669040) and the `work_validate` action (@1680400..1680528). */
+uint64_t npow_work_value(const uint8_t root[32], uint64_t nonce);
+
+/* First-win search: scan the nonce space from `start` on every device in
+ * `device_mask` (device k of G starts at start + k*2^64/G, disjoint strides) until one
+ * value >= threshold is found (NPOW_OK), `*cancel` becomes non-zero
+ * (NPOW_CANCELLED), or every device's stride of `max_nonces_per_device`
+ * (0 = unbounded) is exhausted (NPOW_EXHAUSTED).
+ * Replaces the kernel `nano_work` (nano-work-server.exe @1661643) and the work
+ * server's GPU loop behind `work_generate` (@1673856 reply fields work /
+ * difficulty / multiplier, "Cancelled" @1673856).  Every GPU winner is
+ * re-validated on the CPU before it is returned.
+ * `cancel` may be NULL.  `nonces_done` (may be NULL) receives the number of
+ * nonces hashed by all devices, including the rest of a chunk after the win. */
+int npow_search(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
+                uint64_t max_nonces_per_device, const volatile uint32_t* cancel,
+                uint64_t* nonce_out, uint64_t* value_out, uint64_t* nonces_done);
+
+/* Batched first-win search over n roots (the DPoW burst: many work_generate
+ * requests in flight at once, client/work_handler.py:83-125 per client).
+ * Each root i gets its own threshold and its own cancel word cancel[i]
+ * (cancel itself or any entry may be NULL).  Roots are dealt round-robin over
+ * the devices in device_mask; status_out[i] is NPOW_OK / NPOW_CANCELLED /
+ * NPOW_EXHAUSTED per root.  Returns NPOW_OK or a negative error. */
+int npow_search_batch(const uint8_t* roots, const uint64_t* thresholds, uint32_t n,
+                      uint64_t device_mask, uint64_t max_nonces_per_root,
+                      const volatile uint32_t* const* cancel, uint64_t* nonces_out,
+                      uint64_t* values_out, int32_t* status_out, uint64_t* nonces_done);
+
+/* Exhaustive sweep: every nonce in [start, start+count) (mod 2^64) whose value
+ * >= threshold, written to out[0..min(n,cap)) in ascending (nonce - start)
+ * order; *n_out = exact hit count.  The range is split into contiguous parts
+ * over the devices in device_mask.  Returns NPOW_ERR_CAPACITY when n > cap
+ * (out then holds the first cap hits), NPOW_CANCELLED if *cancel fired. */
+int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t count,
+               uint64_t device_mask, const volatile uint32_t* cancel, uint64_t* out, uint64_t cap,
+               uint64_t* n_out);
+
+/* Work values of `count` consecutive nonces start, start+1, ... for one root,
+ * computed by the same specialised GPU code path the search and sweep kernels
+ * use (parity tests compare every value with the CPU).  device = HIP index. */
+int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t count, uint64_t* values_out);
+
+/* Work values of n independent (root_i, nonce_i) pairs on one device
+ * (generic per-lane-root GPU path; server-side validation in bulk,
+ * dpow_server.py:130,365). */
+int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, uint32_t n,
+                      uint64_t* values_out);
+
+/* Tuning knobs (0 keeps the current value).  iters_per_launch: wave
+ * iterations per kernel launch (chunk = grid*256*iters nonces);
+ * poll_interval: iterations between a wave's polls of the host abort word;
+ * blocks_per_cu: workgroups of 256 lanes per CU in the launch grid. */
+int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t blocks_per_cu);
+
+int npow_device_stats_get(int device, npow_device_stats* out);
+int npow_device_stats_reset(int device);
+
+/* Library / kernel identification string (gfx target, build flags). */
+const char* npow_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NANOPOW_H */

@@ -1,0 +1,645 @@
+// npow_engine.cpp -- host engine of libnanopow.so: devices, streams, chunked
+// launch loop, first-win across GPUs, cancellation, sweeps, C ABI.
+//
+// Replaces the GPU work loop of the reference work server
+// (client/bin/windows/nano-work-server.exe; Rust source not vendored, behaviour
+// from its strings): per request every GPU scans nonce chunks ("THREADS ...
+// defaults to 1048576" @1681064), the host re-validates every GPU result on
+// the CPU ("GPU returned invalid work", @1669040) and gives up on a device
+// after 3 consecutive invalid results (@1669144), and work_cancel stops the
+// search with "Cancelled" (@1673856).
+//
+// MI355X design: one host thread + one HIP stream per GPU, two
+// launches in flight per stream so the next chunk is queued behind the
+// running one, disjoint per-GPU nonce strides, first win published by the
+// kernel into host-coherent pinned memory, and a pinned abort word every wave
+// polls.  No collective: the only cross-GPU datum is the winner.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/nanopow.h"
+#include "npow_blake2b.h"
+#include "npow_internal.h"
+
+namespace npow {
+namespace {
+
+thread_local std::string t_err;
+
+int fail(int code, const std::string& msg) {
+  t_err = msg;
+  return code;
+}
+
+#define HIPTRY(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return fail(NPOW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
+  } while (0)
+
+constexpr int kEventRing = 4;
+constexpr uint64_t kHitCap = 1u << 20;        // per-device sweep hit buffer (8 MiB)
+constexpr uint64_t kValuesChunk = 1u << 24;   // values mode: nonces per launch (128 MiB out)
+
+struct Device {
+  int id = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  DevState* st = nullptr;        // device memory
+  HostMailbox* mb = nullptr;     // pinned host (coherent), host view
+  HostMailbox* mb_dev = nullptr; // device view of the same bytes
+  uint64_t* d_out = nullptr;     // sweep hits / values (kValuesChunk entries)
+  hipEvent_t ev_start[kEventRing] = {};
+  hipEvent_t ev_stop[kEventRing] = {};
+  std::mutex mu;                 // one task per device at a time
+  // statistics
+  std::mutex stats_mu;
+  uint64_t launches = 0, nonces = 0, invalid = 0;
+  double kernel_ms = 0.0;
+  bool dead = false;
+};
+
+std::mutex g_mu;
+bool g_init = false;
+std::vector<std::unique_ptr<Device>> g_devs;
+std::atomic<uint32_t> g_iters{64};      // wave iterations per launch
+std::atomic<uint32_t> g_poll{16};       // iterations between host-abort polls (power of two)
+std::atomic<uint32_t> g_blocks_per_cu{8};
+
+int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }
+
+uint32_t poll_mask() {
+  uint32_t p = g_poll.load();
+  uint32_t m = 1;
+  while (m < p) m <<= 1;
+  return m - 1;
+}
+
+void store_release(volatile uint32_t* p, uint32_t v) { __atomic_store_n((uint32_t*)p, v, __ATOMIC_RELEASE); }
+uint32_t load_acquire(const volatile uint32_t* p) { return __atomic_load_n((const uint32_t*)p, __ATOMIC_ACQUIRE); }
+
+void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#endif
+}
+
+std::vector<Device*> select_devices(uint64_t mask) {
+  std::vector<Device*> out;
+  for (auto& d : g_devs)
+    if ((mask == 0 || (mask >> d->id) & 1ull) && !d->dead) out.push_back(d.get());
+  return out;
+}
+
+// One in-flight launch.
+struct Inflight {
+  int ring;
+  uint64_t count;
+};
+
+// Launch one chunk on d's stream bracketed by timing events.
+int launch_chunk(Device& d, Mode mode, const LaunchArgs& a, int ring, uint64_t* out) {
+  HIPTRY(hipEventRecord(d.ev_start[ring], d.stream));
+  HIPTRY(launch_task(mode, grid_of(d), d.stream, a, d.st, d.mb_dev, out));
+  HIPTRY(hipEventRecord(d.ev_stop[ring], d.stream));
+  return NPOW_OK;
+}
+
+void account_launch(Device& d, int ring) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, d.ev_start[ring], d.ev_stop[ring]) != hipSuccess) ms = 0.f;
+  std::lock_guard<std::mutex> g(d.stats_mu);
+  d.launches++;
+  d.kernel_ms += ms;
+}
+
+// Wait for every in-flight launch, accounting its time.
+int drain(Device& d, std::deque<Inflight>& q) {
+  HIPTRY(hipStreamSynchronize(d.stream));
+  while (!q.empty()) {
+    account_launch(d, q.front().ring);
+    q.pop_front();
+  }
+  return NPOW_OK;
+}
+
+int read_state(Device& d, DevState* hs) {
+  HIPTRY(hipMemcpyAsync(hs, d.st, sizeof(DevState), hipMemcpyDeviceToHost, d.stream));
+  HIPTRY(hipStreamSynchronize(d.stream));
+  std::lock_guard<std::mutex> g(d.stats_mu);
+  d.nonces += hs->done;
+  return NPOW_OK;
+}
+
+int reset_task(Device& d) {
+  HIPTRY(hipMemsetAsync(d.st, 0, sizeof(DevState), d.stream));
+  HIPTRY(hipStreamSynchronize(d.stream));
+  store_release(&d.mb->found, 0);
+  store_release(&d.mb->abort, 0);
+  return NPOW_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// First-win search shared by every device of one request.
+struct SharedSearch {
+  std::atomic<int> winner{-1};
+  std::atomic<bool> stop{false};
+  std::atomic<bool> cancelled{false};
+  uint64_t nonce = 0, value = 0;
+  const volatile uint32_t* cancel = nullptr;
+  std::mutex err_mu;
+  int err = NPOW_OK;
+  std::string err_msg;
+  std::atomic<uint64_t> done{0};
+  void set_error(int code, const std::string& m) {
+    std::lock_guard<std::mutex> g(err_mu);
+    if (err == NPOW_OK) {
+      err = code;
+      err_msg = m;
+    }
+    stop = true;
+  }
+};
+
+// Scan this device's stride until a win (here or elsewhere), cancel, or exhaustion.
+int device_search(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t start, uint64_t max_nonces,
+                  SharedSearch& sh) {
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIPTRY(hipSetDevice(d.id));
+  int rc = reset_task(d);
+  if (rc) return rc;
+
+  LaunchArgs a{};
+  a.pre = pre;
+  a.threshold = threshold;
+  a.poll_mask = poll_mask();
+  a.cap = 0;
+  const uint64_t chunk = (uint64_t)grid_of(d) * kBlock * g_iters.load();
+  uint64_t issued = 0;
+  int ring = 0, invalid_streak = 0;
+  std::deque<Inflight> q;
+  uint64_t total_done = 0;
+
+  for (;;) {
+    // keep two chunks queued on the stream
+    while (q.size() < 2 && !sh.stop.load(std::memory_order_relaxed) &&
+           (max_nonces == 0 || issued < max_nonces)) {
+      const uint64_t cnt = max_nonces ? std::min(chunk, max_nonces - issued) : chunk;
+      a.base = start + issued;
+      a.count = cnt;
+      rc = launch_chunk(d, Mode::kSearch, a, ring, nullptr);
+      if (rc) return rc;
+      q.push_back({ring, cnt});
+      ring = (ring + 1) % kEventRing;
+      issued += cnt;
+    }
+    // retire finished launches (FIFO)
+    while (!q.empty() && hipEventQuery(d.ev_stop[q.front().ring]) == hipSuccess) {
+      account_launch(d, q.front().ring);
+      q.pop_front();
+    }
+    // a win published by this GPU?
+    if (load_acquire(&d.mb->found)) {
+      const uint64_t n = __atomic_load_n(&d.mb->nonce, __ATOMIC_ACQUIRE);
+      const uint64_t v = __atomic_load_n(&d.mb->value, __ATOMIC_ACQUIRE);
+      const uint64_t cpu_v = host_work_value(pre.m, n);
+      if (cpu_v == v && v >= threshold) {
+        int expected = -1;
+        if (sh.winner.compare_exchange_strong(expected, d.id)) {
+          sh.nonce = n;
+          sh.value = v;
+        }
+        sh.stop = true;
+      } else {
+        // "GPU returned invalid work" -- re-arm and keep searching; give up after 3 in a row.
+        {
+          std::lock_guard<std::mutex> g(d.stats_mu);
+          d.invalid++;
+        }
+        fprintf(stderr, "nanopow: GPU %d returned invalid work %016llx (value %016llx, cpu %016llx)\n", d.id,
+                (unsigned long long)n, (unsigned long long)v, (unsigned long long)cpu_v);
+        rc = drain(d, q);
+        if (rc) return rc;
+        DevState hs;
+        rc = read_state(d, &hs);
+        if (rc) return rc;
+        total_done += hs.done;
+        if (++invalid_streak >= 3) {
+          d.dead = true;
+          sh.done += total_done;
+          return fail(NPOW_ERR_INVALID_WORK,
+                      "GPU " + std::to_string(d.id) +
+                          " returned invalid work 3 consecutive times, abandoning it for this work");
+        }
+        rc = reset_task(d);
+        if (rc) return rc;
+        continue;
+      }
+    }
+    if (!sh.stop.load(std::memory_order_relaxed) && sh.cancel && load_acquire(sh.cancel)) {
+      sh.cancelled = true;
+      sh.stop = true;
+    }
+    if (sh.stop.load(std::memory_order_relaxed)) {
+      store_release(&d.mb->abort, 1);
+      break;
+    }
+    if (q.empty() && max_nonces && issued >= max_nonces) break;  // stride exhausted
+    cpu_relax();
+  }
+  rc = drain(d, q);
+  if (rc) return rc;
+  // a win may have landed in the last chunk of an exhausted stride
+  if (!sh.stop.load() && load_acquire(&d.mb->found)) {
+    const uint64_t n = __atomic_load_n(&d.mb->nonce, __ATOMIC_ACQUIRE);
+    const uint64_t v = __atomic_load_n(&d.mb->value, __ATOMIC_ACQUIRE);
+    if (host_work_value(pre.m, n) == v && v >= threshold) {
+      int expected = -1;
+      if (sh.winner.compare_exchange_strong(expected, d.id)) {
+        sh.nonce = n;
+        sh.value = v;
+      }
+      sh.stop = true;
+    }
+  }
+  DevState hs;
+  rc = read_state(d, &hs);
+  if (rc) return rc;
+  total_done += hs.done;
+  sh.done += total_done;
+  return NPOW_OK;
+}
+
+template <class F>
+void run_on_devices(const std::vector<Device*>& devs, F&& fn) {
+  if (devs.size() == 1) {
+    fn(0, *devs[0]);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(devs.size());
+  for (size_t k = 0; k < devs.size(); ++k) th.emplace_back([&, k] { fn(k, *devs[k]); });
+  for (auto& t : th) t.join();
+}
+
+int check_init() {
+  if (!g_init) return fail(NPOW_ERR_NOT_INITIALISED, "npow_init() has not been called");
+  return NPOW_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// Sweep one contiguous sub-range on one device; hits (unsorted) appended to `hits`.
+int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t start, uint64_t count,
+                 const volatile uint32_t* cancel, std::vector<uint64_t>& hits, uint64_t& n_total,
+                 bool& cancelled) {
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIPTRY(hipSetDevice(d.id));
+  int rc = reset_task(d);
+  if (rc) return rc;
+  LaunchArgs a{};
+  a.pre = pre;
+  a.threshold = threshold;
+  a.poll_mask = poll_mask();
+  a.cap = (uint32_t)kHitCap;
+  const uint64_t chunk = (uint64_t)grid_of(d) * kBlock * g_iters.load();
+  uint64_t issued = 0;
+  int ring = 0;
+  std::deque<Inflight> q;
+  cancelled = false;
+  while (issued < count || !q.empty()) {
+    while (q.size() < 2 && issued < count && !cancelled) {
+      const uint64_t cnt = std::min(chunk, count - issued);
+      a.base = start + issued;
+      a.count = cnt;
+      rc = launch_chunk(d, Mode::kSweep, a, ring, d.d_out);
+      if (rc) return rc;
+      q.push_back({ring, cnt});
+      ring = (ring + 1) % kEventRing;
+      issued += cnt;
+    }
+    while (!q.empty() && hipEventQuery(d.ev_stop[q.front().ring]) == hipSuccess) {
+      account_launch(d, q.front().ring);
+      q.pop_front();
+    }
+    if (!cancelled && cancel && load_acquire(cancel)) {
+      cancelled = true;
+      store_release(&d.mb->abort, 1);
+    }
+    if (cancelled && q.empty()) break;
+    if (q.size() >= 2 || (issued >= count && !q.empty())) std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+  rc = drain(d, q);
+  if (rc) return rc;
+  DevState hs;
+  rc = read_state(d, &hs);
+  if (rc) return rc;
+  n_total = hs.n_hits;
+  const uint64_t k = std::min<uint64_t>(hs.n_hits, kHitCap);
+  hits.resize(k);
+  if (k) {
+    HIPTRY(hipMemcpy(hits.data(), d.d_out, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  }
+  return NPOW_OK;
+}
+
+}  // namespace
+}  // namespace npow
+
+using namespace npow;
+
+extern "C" {
+
+const char* npow_last_error(void) { return t_err.c_str(); }
+
+const char* npow_version(void) {
+  return "libnanopow 0.1 (gfx950 HIP kernel: blake2b-64 nonce search; v_lshl_add_u64 adds, v_alignbit rotations)";
+}
+
+int npow_init(int* n_devices) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_init) {
+    if (n_devices) *n_devices = (int)g_devs.size();
+    return NPOW_OK;
+  }
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0)
+    return fail(NPOW_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
+  for (int i = 0; i < n && i < 64; ++i) {
+    auto d = std::make_unique<Device>();
+    d->id = i;
+    HIPTRY(hipSetDevice(i));
+    hipDeviceProp_t p;
+    HIPTRY(hipGetDeviceProperties(&p, i));
+    d->cus = p.multiProcessorCount;
+    HIPTRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
+    HIPTRY(hipMalloc(&d->st, sizeof(DevState)));
+    HIPTRY(hipMalloc(&d->d_out, kValuesChunk * sizeof(uint64_t)));
+    void* mb = nullptr;
+    HIPTRY(hipHostMalloc(&mb, sizeof(HostMailbox), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+    memset(mb, 0, sizeof(HostMailbox));
+    d->mb = (HostMailbox*)mb;
+    void* mbd = nullptr;
+    HIPTRY(hipHostGetDevicePointer(&mbd, mb, 0));
+    d->mb_dev = (HostMailbox*)mbd;
+    for (int r = 0; r < kEventRing; ++r) {
+      HIPTRY(hipEventCreate(&d->ev_start[r]));
+      HIPTRY(hipEventCreate(&d->ev_stop[r]));
+    }
+    g_devs.push_back(std::move(d));
+  }
+  g_init = true;
+  if (n_devices) *n_devices = (int)g_devs.size();
+  return NPOW_OK;
+}
+
+void npow_shutdown(void) {
+  std::lock_guard<std::mutex> g(g_mu);
+  for (auto& d : g_devs) {
+    std::lock_guard<std::mutex> lk(d->mu);
+    (void)hipSetDevice(d->id);
+    (void)hipStreamSynchronize(d->stream);
+    for (int r = 0; r < kEventRing; ++r) {
+      (void)hipEventDestroy(d->ev_start[r]);
+      (void)hipEventDestroy(d->ev_stop[r]);
+    }
+    (void)hipFree(d->st);
+    (void)hipFree(d->d_out);
+    (void)hipHostFree(d->mb);
+    (void)hipStreamDestroy(d->stream);
+  }
+  g_devs.clear();
+  g_init = false;
+}
+
+uint64_t npow_work_value(const uint8_t root[32], uint64_t nonce) {
+  uint64_t m[4];
+  for (int i = 0; i < 4; ++i) m[i] = host_load_le64(root + 8 * i);
+  return host_work_value(m, nonce);
+}
+
+int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t blocks_per_cu) {
+  if (iters_per_launch) g_iters = iters_per_launch;
+  if (poll_interval) g_poll = poll_interval;
+  if (blocks_per_cu) {
+    if (blocks_per_cu > 32) return fail(NPOW_ERR_BAD_ARGUMENT, "blocks_per_cu must be <= 32");
+    g_blocks_per_cu = blocks_per_cu;
+  }
+  return NPOW_OK;
+}
+
+int npow_device_stats_get(int device, npow_device_stats* out) {
+  if (int rc = check_init()) return rc;
+  if (device < 0 || device >= (int)g_devs.size() || !out) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
+  Device& d = *g_devs[device];
+  std::lock_guard<std::mutex> g(d.stats_mu);
+  out->launches = d.launches;
+  out->nonces = d.nonces;
+  out->kernel_ms = d.kernel_ms;
+  out->invalid_work = d.invalid;
+  out->cus = d.cus;
+  out->grid = grid_of(d);
+  return NPOW_OK;
+}
+
+int npow_device_stats_reset(int device) {
+  if (int rc = check_init()) return rc;
+  if (device < 0 || device >= (int)g_devs.size()) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
+  Device& d = *g_devs[device];
+  std::lock_guard<std::mutex> g(d.stats_mu);
+  d.launches = d.nonces = d.invalid = 0;
+  d.kernel_ms = 0.0;
+  return NPOW_OK;
+}
+
+int npow_search(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
+                uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* nonce_out,
+                uint64_t* value_out, uint64_t* nonces_done) {
+  if (int rc = check_init()) return rc;
+  if (!root || !nonce_out) return fail(NPOW_ERR_BAD_ARGUMENT, "root and nonce_out are required");
+  auto devs = select_devices(device_mask);
+  if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable device in device_mask");
+  const RootPrecomp pre = host_precompute(root);
+  SharedSearch sh;
+  sh.cancel = cancel;
+  const uint64_t G = devs.size();
+  const uint64_t spacing = G > 1 ? (~0ull / G) + 1 : 0;  // 2^64 / G (exact for powers of two)
+  run_on_devices(devs, [&](size_t k, Device& d) {
+    int rc = device_search(d, pre, threshold, start + k * spacing, max_nonces_per_device, sh);
+    if (rc) sh.set_error(rc, t_err);
+  });
+  if (nonces_done) *nonces_done = sh.done.load();
+  if (sh.winner.load() >= 0) {
+    *nonce_out = sh.nonce;
+    if (value_out) *value_out = sh.value;
+    return NPOW_OK;
+  }
+  if (sh.err != NPOW_OK) return fail(sh.err, sh.err_msg);
+  if (sh.cancelled.load()) return NPOW_CANCELLED;
+  return NPOW_EXHAUSTED;
+}
+
+int npow_search_batch(const uint8_t* roots, const uint64_t* thresholds, uint32_t n, uint64_t device_mask,
+                      uint64_t max_nonces_per_root, const volatile uint32_t* const* cancel, uint64_t* nonces_out,
+                      uint64_t* values_out, int32_t* status_out, uint64_t* nonces_done) {
+  if (int rc = check_init()) return rc;
+  if (n == 0) return NPOW_OK;
+  if (!roots || !thresholds || !nonces_out || !status_out)
+    return fail(NPOW_ERR_BAD_ARGUMENT, "roots, thresholds, nonces_out and status_out are required");
+  auto devs = select_devices(device_mask);
+  if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable device in device_mask");
+  std::atomic<uint64_t> done{0};
+  std::mutex err_mu;
+  int err = NPOW_OK;
+  std::string err_msg;
+  run_on_devices(devs, [&](size_t k, Device& d) {
+    for (uint32_t i = (uint32_t)k; i < n; i += (uint32_t)devs.size()) {
+      const RootPrecomp pre = host_precompute(roots + 32 * (size_t)i);
+      SharedSearch sh;
+      sh.cancel = cancel ? cancel[i] : nullptr;
+      // distinct start per root: derived from the root so repeated roots restart identically
+      const uint64_t start = pre.m[0] ^ pre.m[3];
+      int rc = device_search(d, pre, thresholds[i], start, max_nonces_per_root, sh);
+      done += sh.done.load();
+      if (rc) {
+        std::lock_guard<std::mutex> g(err_mu);
+        if (err == NPOW_OK) {
+          err = rc;
+          err_msg = t_err;
+        }
+        status_out[i] = rc;
+        continue;
+      }
+      if (sh.winner.load() >= 0) {
+        nonces_out[i] = sh.nonce;
+        if (values_out) values_out[i] = sh.value;
+        status_out[i] = NPOW_OK;
+      } else {
+        status_out[i] = sh.cancelled.load() ? NPOW_CANCELLED : NPOW_EXHAUSTED;
+      }
+    }
+  });
+  if (nonces_done) *nonces_done = done.load();
+  if (err != NPOW_OK) return fail(err, err_msg);
+  return NPOW_OK;
+}
+
+int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t count, uint64_t device_mask,
+               const volatile uint32_t* cancel, uint64_t* out, uint64_t cap, uint64_t* n_out) {
+  if (int rc = check_init()) return rc;
+  if (!root || !n_out || (cap && !out)) return fail(NPOW_ERR_BAD_ARGUMENT, "root, n_out (and out when cap>0) required");
+  auto devs = select_devices(device_mask);
+  if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable device in device_mask");
+  const RootPrecomp pre = host_precompute(root);
+  const size_t G = devs.size();
+  std::vector<std::vector<uint64_t>> hits(G);
+  std::vector<uint64_t> totals(G, 0);
+  std::vector<int> rcs(G, 0);
+  std::vector<std::string> msgs(G);
+  std::vector<char> canc(G, 0);
+  const uint64_t per = count / G, rem = count % G;
+  std::vector<uint64_t> sub_start(G), sub_count(G);
+  uint64_t off = 0;
+  for (size_t k = 0; k < G; ++k) {
+    sub_start[k] = start + off;
+    sub_count[k] = per + (k < rem ? 1 : 0);
+    off += sub_count[k];
+  }
+  run_on_devices(devs, [&](size_t k, Device& d) {
+    bool c = false;
+    rcs[k] = device_sweep(d, pre, threshold, sub_start[k], sub_count[k], cancel, hits[k], totals[k], c);
+    canc[k] = c;
+    if (rcs[k]) msgs[k] = t_err;
+  });
+  for (size_t k = 0; k < G; ++k)
+    if (rcs[k]) return fail(rcs[k], msgs[k]);
+  uint64_t total = 0;
+  bool overflow = false;
+  std::vector<uint64_t> all;
+  for (size_t k = 0; k < G; ++k) {
+    total += totals[k];
+    if (totals[k] > hits[k].size()) overflow = true;
+    all.insert(all.end(), hits[k].begin(), hits[k].end());
+  }
+  std::sort(all.begin(), all.end(), [start](uint64_t x, uint64_t y) { return x - start < y - start; });
+  const uint64_t k = std::min<uint64_t>(all.size(), cap);
+  if (k) memcpy(out, all.data(), k * sizeof(uint64_t));
+  *n_out = total;
+  for (size_t j = 0; j < G; ++j)
+    if (canc[j]) return NPOW_CANCELLED;
+  if (overflow) return fail(NPOW_ERR_CAPACITY, "device hit buffer overflow (more than 2^20 hits per device)");
+  if (total > cap) return fail(NPOW_ERR_CAPACITY, "more hits than cap");
+  return NPOW_OK;
+}
+
+int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t count, uint64_t* values_out) {
+  if (int rc = check_init()) return rc;
+  if (device < 0 || device >= (int)g_devs.size() || !root || (count && !values_out))
+    return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
+  Device& d = *g_devs[device];
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIPTRY(hipSetDevice(d.id));
+  int rc = reset_task(d);
+  if (rc) return rc;
+  LaunchArgs a{};
+  a.pre = host_precompute(root);
+  a.poll_mask = 0;
+  for (uint64_t off = 0; off < count; off += kValuesChunk) {
+    const uint64_t cnt = std::min(kValuesChunk, count - off);
+    a.base = start + off;
+    a.count = cnt;
+    rc = launch_chunk(d, Mode::kValues, a, 0, d.d_out);
+    if (rc) return rc;
+    HIPTRY(hipMemcpyAsync(values_out + off, d.d_out, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+    HIPTRY(hipStreamSynchronize(d.stream));
+    account_launch(d, 0);
+  }
+  DevState hs;
+  return read_state(d, &hs);
+}
+
+int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, uint32_t n, uint64_t* values_out) {
+  if (int rc = check_init()) return rc;
+  if (device < 0 || device >= (int)g_devs.size() || (n && (!roots || !nonces || !values_out)))
+    return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
+  if (n == 0) return NPOW_OK;
+  Device& d = *g_devs[device];
+  std::lock_guard<std::mutex> lk(d.mu);
+  HIPTRY(hipSetDevice(d.id));
+  std::vector<uint64_t> words((size_t)n * 4);
+  for (uint32_t i = 0; i < n; ++i)
+    for (int k = 0; k < 4; ++k) words[4 * (size_t)i + k] = host_load_le64(roots + 32 * (size_t)i + 8 * k);
+  uint64_t *dw = nullptr, *dn = nullptr, *dv = nullptr;
+  HIPTRY(hipMalloc(&dw, words.size() * 8));
+  HIPTRY(hipMalloc(&dn, (size_t)n * 8));
+  HIPTRY(hipMalloc(&dv, (size_t)n * 8));
+  int rc = NPOW_OK;
+  do {
+    hipError_t e;
+    if ((e = hipMemcpy(dw, words.data(), words.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = hipMemcpy(dn, nonces, (size_t)n * 8, hipMemcpyHostToDevice)) != hipSuccess ||
+        (e = launch_pairs((int)((n + kBlock - 1) / kBlock), d.stream, dw, dn, n, dv)) != hipSuccess ||
+        (e = hipStreamSynchronize(d.stream)) != hipSuccess ||
+        (e = hipMemcpy(values_out, dv, (size_t)n * 8, hipMemcpyDeviceToHost)) != hipSuccess) {
+      rc = fail(NPOW_ERR_HIP, std::string("values_pairs: ") + hipGetErrorString(e));
+    }
+  } while (0);
+  (void)hipFree(dw);
+  (void)hipFree(dn);
+  (void)hipFree(dv);
+  return rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,227 @@
+// npow_kernel.hip -- gfx950 (MI355X / CDNA4) kernels of the Nano proof-of-work engine.
+//
+// Replaces the OpenCL kernel `nano_work` + inline `blake2b()` embedded in the
+// reference work server (client/bin/windows/nano-work-server.exe @1657474..1661900).
+// Written from the BLAKE2b definition for the gfx950 VALU, not translated:
+//
+//  * One nonce per lane, the 16-word state in VGPRs, rounds fully unrolled with
+//    the message schedule resolved at compile time: 11 of the 16 message words
+//    are zero, so their adds vanish; m1..m4 (the root) are uniform kernel
+//    arguments held in SGPRs.
+//  * 64-bit adds are single `v_lshl_add_u64` instructions (measured: one
+//    64-bit add per 4.4 SIMD cycles, the cost of ONE v_add_co_u32, half the
+//    v_add_co/v_addc pair -- profiles/r01_valu_ubench.json).
+//  * Rotations are split into 32-bit halves: rotr32 is a free register swap,
+//    rotr24 / rotr16 / rotr63 are two `v_alignbit_b32` each.
+//  * Round 1's three nonce-independent column steps are precomputed per root
+//    on the host (RootPrecomp) and arrive in SGPRs.  Dead work of round 12
+//    (only v0 and v8 feed the digest word) is removed by the compiler.
+//  * Grid-stride loop over the launch's nonce range; the hit test is a wave
+//    ballot, so a wave leaves the fast path only when one of its 64 lanes wins.
+//  * Search mode: first win by atomicCAS on a device slot, published to a
+//    host-coherent mailbox with system-scope stores; every wave polls the
+//    device slot each iteration (agent-scope load, L2) and the host abort
+//    word every poll_mask+1 iterations (system-scope load).
+//  * Sweep mode: every hit appended through an atomic counter (order-free;
+//    the host sorts).  Values mode: writes every value (parity tests).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "npow_internal.h"
+
+namespace npow {
+
+// ---- 64-bit rotations on 32-bit halves --------------------------------------------------
+__device__ __forceinline__ uint64_t pack(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+
+__device__ __forceinline__ uint64_t rotr32(uint64_t x) {  // register swap, no instruction
+  return pack((uint32_t)(x >> 32), (uint32_t)x);
+}
+template <int N>  // 0 < N < 32
+__device__ __forceinline__ uint64_t rotr_lt32(uint64_t x) {
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return pack(__builtin_amdgcn_alignbit(hi, lo, N), __builtin_amdgcn_alignbit(lo, hi, N));
+}
+__device__ __forceinline__ uint64_t rotr63(uint64_t x) {  // = rotl 1
+  const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  return pack(__builtin_amdgcn_alignbit(lo, hi, 31), __builtin_amdgcn_alignbit(hi, lo, 31));
+}
+
+// ---- message words: m0 = nonce, m1..m4 = root, the rest zero (resolved at compile time) --
+template <int I>
+__device__ __forceinline__ uint64_t add_msg(uint64_t a, uint64_t nonce, const uint64_t (&m)[4]) {
+  if constexpr (I == 0) return a + nonce;
+  else if constexpr (I <= 4) return a + m[I - 1];
+  else return a;
+}
+
+template <int X, int Y>
+__device__ __forceinline__ void G(uint64_t& a, uint64_t& b, uint64_t& c, uint64_t& d, uint64_t n,
+                                  const uint64_t (&m)[4]) {
+  a = add_msg<X>(a, n, m) + b;
+  d = rotr32(d ^ a);
+  c = c + d;
+  b = rotr_lt32<24>(b ^ c);
+  a = add_msg<Y>(a, n, m) + b;
+  d = rotr_lt32<16>(d ^ a);
+  c = c + d;
+  b = rotr63(b ^ c);
+}
+
+template <int R>
+__device__ __forceinline__ void columns(uint64_t (&v)[16], uint64_t n, const uint64_t (&m)[4]) {
+  G<kSigma[R][0], kSigma[R][1]>(v[0], v[4], v[8], v[12], n, m);
+  G<kSigma[R][2], kSigma[R][3]>(v[1], v[5], v[9], v[13], n, m);
+  G<kSigma[R][4], kSigma[R][5]>(v[2], v[6], v[10], v[14], n, m);
+  G<kSigma[R][6], kSigma[R][7]>(v[3], v[7], v[11], v[15], n, m);
+}
+template <int R>
+__device__ __forceinline__ void diagonals(uint64_t (&v)[16], uint64_t n, const uint64_t (&m)[4]) {
+  G<kSigma[R][8], kSigma[R][9]>(v[0], v[5], v[10], v[15], n, m);
+  G<kSigma[R][10], kSigma[R][11]>(v[1], v[6], v[11], v[12], n, m);
+  G<kSigma[R][12], kSigma[R][13]>(v[2], v[7], v[8], v[13], n, m);
+  G<kSigma[R][14], kSigma[R][15]>(v[3], v[4], v[9], v[14], n, m);
+}
+
+template <int R>
+__device__ __forceinline__ void rounds_from(uint64_t (&v)[16], uint64_t n, const uint64_t (&m)[4]) {
+  if constexpr (R < 12) {
+    columns<R>(v, n, m);
+    diagonals<R>(v, n, m);
+    rounds_from<R + 1>(v, n, m);
+  }
+}
+
+// Work value with round 1's nonce-independent columns taken from `col` (uniform).
+__device__ __forceinline__ uint64_t work_value_pre(uint64_t nonce, const uint64_t (&m)[4],
+                                                   const uint64_t (&col)[12]) {
+  uint64_t v[16];
+  v[0] = kH0;
+  v[4] = kIV4;
+  v[8] = kIV0;
+  v[12] = kV12;
+  G<0, 1>(v[0], v[4], v[8], v[12], nonce, m);  // round-1 column 0: the only nonce-dependent one
+  v[1] = col[0]; v[5] = col[1]; v[9] = col[2];  v[13] = col[3];
+  v[2] = col[4]; v[6] = col[5]; v[10] = col[6]; v[14] = col[7];
+  v[3] = col[8]; v[7] = col[9]; v[11] = col[10]; v[15] = col[11];
+  diagonals<0>(v, nonce, m);
+  rounds_from<1>(v, nonce, m);
+  return kH0 ^ v[0] ^ v[8];
+}
+
+// Generic work value (per-lane root): all 12 rounds on the GPU.
+__device__ __forceinline__ uint64_t work_value_full(uint64_t nonce, const uint64_t (&m)[4]) {
+  uint64_t v[16] = {kH0, kIV1, kIV2, kIV3, kIV4, kIV5, kIV6, kIV7,
+                    kIV0, kIV1, kIV2, kIV3, kV12, kIV5, kV14, kIV7};
+  rounds_from<0>(v, nonce, m);
+  return kH0 ^ v[0] ^ v[8];
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, int lane) {
+  const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, lane);
+  const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), lane);
+  return pack(lo, hi);
+}
+
+template <Mode MODE>
+__global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, DevState* __restrict__ st,
+                                                             HostMailbox* __restrict__ mb,
+                                                             uint64_t* __restrict__ out) {
+  // Uniform copies (the compiler keeps kernel arguments in SGPRs).
+  uint64_t m[4], col[12];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) m[i] = a.pre.m[i];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) col[i] = a.pre.col[i];
+
+  const uint32_t lane = threadIdx.x & 63;
+  // First lane index of this wave; wave-uniform.
+  const uint64_t wave0 =
+      (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kBlock + (threadIdx.x & ~63u));
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  uint64_t done = 0;  // nonces this wave hashed (wave-uniform)
+  uint32_t iter = 0;
+
+  for (uint64_t ib = wave0; ib < a.count; ib += stride, ++iter) {
+    // Issue the early-exit polls first; their latency hides under the hash.
+    uint32_t stop = 0;
+    if constexpr (MODE == Mode::kSearch)
+      stop = __hip_atomic_load(&st->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if constexpr (MODE != Mode::kValues) {
+      if ((iter & a.poll_mask) == 0)
+        stop |= __hip_atomic_load(&mb->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+
+    const uint64_t i = ib + lane;
+    const uint64_t nonce = a.base + i;
+    const uint64_t value = work_value_pre(nonce, m, col);
+    const bool in_range = i < a.count;
+    const uint64_t rem = a.count - ib;
+    done += rem < 64 ? rem : 64;
+
+    if constexpr (MODE == Mode::kValues) {
+      if (in_range) out[i] = value;
+    } else {
+      const bool hit = in_range && value >= a.threshold;
+      const uint64_t hits = __ballot(hit);
+      if (__builtin_expect(hits != 0, 0)) {
+        if constexpr (MODE == Mode::kSearch) {
+          const int w = __builtin_ctzll(hits);
+          const uint64_t wn = readlane64(nonce, w), wv = readlane64(value, w);
+          if (lane == 0) {
+            if (atomicCAS(&st->found, 0u, 1u) == 0u) {
+              st->nonce = wn;
+              st->value = wv;
+              __hip_atomic_store(&mb->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(&mb->value, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              __hip_atomic_store(&mb->found, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+            }
+          }
+          break;
+        } else {  // sweep: append every hit
+          if (hit) {
+            const uint32_t slot = atomicAdd(&st->n_hits, 1u);
+            if (slot < a.cap) out[slot] = nonce;
+          }
+        }
+      }
+      if (__builtin_amdgcn_readfirstlane(stop)) break;
+    }
+  }
+  if (lane == 0 && done) atomicAdd(&st->done, (unsigned long long)done);
+}
+
+__global__ __launch_bounds__(kBlock) void npow_pairs_kernel(const uint64_t* __restrict__ roots_words,
+                                                            const uint64_t* __restrict__ nonces, uint32_t n,
+                                                            uint64_t* __restrict__ out) {
+  const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+  if (i >= n) return;
+  uint64_t m[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m[k] = roots_words[4 * (size_t)i + k];
+  out[i] = work_value_full(nonces[i], m);
+}
+
+hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs& a, DevState* st,
+                       HostMailbox* mb, uint64_t* out) {
+  switch (mode) {
+    case Mode::kSearch:
+      npow_task_kernel<Mode::kSearch><<<grid, kBlock, 0, stream>>>(a, st, mb, out);
+      break;
+    case Mode::kSweep:
+      npow_task_kernel<Mode::kSweep><<<grid, kBlock, 0, stream>>>(a, st, mb, out);
+      break;
+    case Mode::kValues:
+      npow_task_kernel<Mode::kValues><<<grid, kBlock, 0, stream>>>(a, st, mb, out);
+      break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_pairs(int grid, hipStream_t stream, const uint64_t* roots_words, const uint64_t* nonces,
+                        uint32_t n, uint64_t* out) {
+  npow_pairs_kernel<<<grid, kBlock, 0, stream>>>(roots_words, nonces, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace npow

@@ -1,0 +1,253 @@
+"""ctypes binding of libnanopow.so (the C ABI declared in include/nanopow.h).
+
+The product path has no CPU fallback: if the HIP library is missing, or no
+GPU is visible, every entry point here raises :class:`NanoPowError`.  ctypes
+releases the GIL for the duration of each foreign call, so searches can run in
+worker threads while the HTTP server keeps serving ``work_cancel``
+(client/work_handler.py:61-80 sends it on a second connection while a
+``work_generate`` is pending).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("NANOPOW_LIB", os.path.join(_HERE, "libnanopow.so"))
+
+NPOW_OK = 0
+NPOW_CANCELLED = 1
+NPOW_EXHAUSTED = 2
+NPOW_ERR_NOT_INITIALISED = -1
+NPOW_ERR_NO_DEVICE = -2
+NPOW_ERR_BAD_ARGUMENT = -3
+NPOW_ERR_HIP = -4
+NPOW_ERR_INVALID_WORK = -5
+NPOW_ERR_CAPACITY = -6
+
+M64 = (1 << 64) - 1
+
+# Every symbol include/nanopow.h declares (tests/test_abi.py checks the export table).
+EXPORTED_SYMBOLS = (
+    "npow_init", "npow_shutdown", "npow_last_error", "npow_work_value", "npow_search",
+    "npow_search_batch", "npow_sweep", "npow_values", "npow_values_pairs", "npow_set_tuning",
+    "npow_device_stats_get", "npow_device_stats_reset", "npow_version",
+)
+
+
+class NanoPowError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"nanopow error {code}: {message}")
+        self.code = code
+        self.message = message
+
+
+class DeviceStats(ctypes.Structure):
+    _fields_ = [
+        ("launches", ctypes.c_uint64),
+        ("nonces", ctypes.c_uint64),
+        ("kernel_ms", ctypes.c_double),
+        ("invalid_work", ctypes.c_uint64),
+        ("cus", ctypes.c_int32),
+        ("grid", ctypes.c_int32),
+    ]
+
+
+@dataclass
+class SearchResult:
+    status: int            # NPOW_OK / NPOW_CANCELLED / NPOW_EXHAUSTED
+    nonce: Optional[int]
+    value: Optional[int]
+    nonces_done: int
+
+
+_lib: Optional[ctypes.CDLL] = None
+_lib_lock = threading.Lock()
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load libnanopow.so and declare every prototype (no device is touched)."""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise NanoPowError(NPOW_ERR_NOT_INITIALISED,
+                               f"{path} not built: run `make -C nano-dpow_amd/csrc` "
+                               "(or __graft_entry__.build())")
+        lib = ctypes.CDLL(path)
+        u8p = ctypes.c_char_p
+        u64, u32 = ctypes.c_uint64, ctypes.c_uint32
+        pu64 = ctypes.POINTER(ctypes.c_uint64)
+        p = ctypes.c_void_p
+        lib.npow_init.argtypes = [ctypes.POINTER(ctypes.c_int)]
+        lib.npow_init.restype = ctypes.c_int
+        lib.npow_shutdown.argtypes = []
+        lib.npow_shutdown.restype = None
+        lib.npow_last_error.argtypes = []
+        lib.npow_last_error.restype = ctypes.c_char_p
+        lib.npow_version.argtypes = []
+        lib.npow_version.restype = ctypes.c_char_p
+        lib.npow_work_value.argtypes = [u8p, u64]
+        lib.npow_work_value.restype = u64
+        lib.npow_search.argtypes = [u8p, u64, u64, u64, u64, p, pu64, pu64, pu64]
+        lib.npow_search.restype = ctypes.c_int
+        lib.npow_search_batch.argtypes = [u8p, p, u32, u64, u64, p, p, p, p, pu64]
+        lib.npow_search_batch.restype = ctypes.c_int
+        lib.npow_sweep.argtypes = [u8p, u64, u64, u64, u64, p, p, u64, pu64]
+        lib.npow_sweep.restype = ctypes.c_int
+        lib.npow_values.argtypes = [ctypes.c_int, u8p, u64, u64, p]
+        lib.npow_values.restype = ctypes.c_int
+        lib.npow_values_pairs.argtypes = [ctypes.c_int, u8p, p, u32, p]
+        lib.npow_values_pairs.restype = ctypes.c_int
+        lib.npow_set_tuning.argtypes = [u32, u32, u32]
+        lib.npow_set_tuning.restype = ctypes.c_int
+        lib.npow_device_stats_get.argtypes = [ctypes.c_int, ctypes.POINTER(DeviceStats)]
+        lib.npow_device_stats_get.restype = ctypes.c_int
+        lib.npow_device_stats_reset.argtypes = [ctypes.c_int]
+        lib.npow_device_stats_reset.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def _check(rc: int, lib: ctypes.CDLL, ok=(NPOW_OK,)) -> int:
+    if rc in ok:
+        return rc
+    msg = lib.npow_last_error()
+    raise NanoPowError(rc, msg.decode("utf-8", "replace") if msg else "")
+
+
+def _root(root: bytes) -> bytes:
+    if not isinstance(root, (bytes, bytearray)) or len(root) != 32:
+        raise ValueError("root must be 32 bytes")
+    return bytes(root)
+
+
+class CancelToken:
+    """A caller-owned 32-bit word the engine polls; set() stops a running search."""
+
+    def __init__(self) -> None:
+        self._word = ctypes.c_uint32(0)
+
+    def set(self) -> None:
+        self._word.value = 1
+
+    def clear(self) -> None:
+        self._word.value = 0
+
+    @property
+    def is_set(self) -> bool:
+        return bool(self._word.value)
+
+    @property
+    def address(self) -> int:
+        return ctypes.addressof(self._word)
+
+
+class Engine:
+    """Thin object wrapper over the C ABI (one per process is enough)."""
+
+    def __init__(self, path: str = LIB_PATH) -> None:
+        self.lib = load(path)
+        n = ctypes.c_int(0)
+        _check(self.lib.npow_init(ctypes.byref(n)), self.lib)
+        self.n_devices = n.value
+
+    # -- CPU helpers -------------------------------------------------------------------
+    def work_value(self, root: bytes, nonce: int) -> int:
+        return int(self.lib.npow_work_value(_root(root), nonce & M64))
+
+    # -- GPU paths ---------------------------------------------------------------------
+    def search(self, root: bytes, threshold: int, start: int = 0, device_mask: int = 0,
+               max_nonces_per_device: int = 0, cancel: Optional[CancelToken] = None) -> SearchResult:
+        nonce = ctypes.c_uint64(0)
+        value = ctypes.c_uint64(0)
+        done = ctypes.c_uint64(0)
+        rc = self.lib.npow_search(_root(root), threshold & M64, start & M64, device_mask,
+                                  max_nonces_per_device, cancel.address if cancel else None,
+                                  ctypes.byref(nonce), ctypes.byref(value), ctypes.byref(done))
+        _check(rc, self.lib, ok=(NPOW_OK, NPOW_CANCELLED, NPOW_EXHAUSTED))
+        if rc == NPOW_OK:
+            return SearchResult(rc, nonce.value, value.value, done.value)
+        return SearchResult(rc, None, None, done.value)
+
+    def search_batch(self, roots: Sequence[bytes], thresholds: Sequence[int], device_mask: int = 0,
+                     max_nonces_per_root: int = 0,
+                     cancels: Optional[Sequence[Optional[CancelToken]]] = None) -> Tuple[List[SearchResult], int]:
+        n = len(roots)
+        if len(thresholds) != n:
+            raise ValueError("roots and thresholds differ in length")
+        rb = b"".join(_root(r) for r in roots)
+        th = (ctypes.c_uint64 * n)(*[t & M64 for t in thresholds])
+        nonces = (ctypes.c_uint64 * n)()
+        values = (ctypes.c_uint64 * n)()
+        status = (ctypes.c_int32 * n)()
+        done = ctypes.c_uint64(0)
+        cptr = None
+        if cancels is not None:
+            arr = (ctypes.c_void_p * n)(*[(c.address if c else None) for c in cancels])
+            cptr = ctypes.addressof(arr)
+        rc = self.lib.npow_search_batch(rb, ctypes.addressof(th), n, device_mask, max_nonces_per_root, cptr,
+                                        ctypes.addressof(nonces), ctypes.addressof(values),
+                                        ctypes.addressof(status), ctypes.byref(done))
+        _check(rc, self.lib)
+        out = []
+        for i in range(n):
+            if status[i] == NPOW_OK:
+                out.append(SearchResult(NPOW_OK, nonces[i], values[i], 0))
+            else:
+                out.append(SearchResult(status[i], None, None, 0))
+        return out, done.value
+
+    def sweep(self, root: bytes, threshold: int, start: int, count: int, device_mask: int = 0,
+              cap: int = 1 << 16, cancel: Optional[CancelToken] = None) -> List[int]:
+        out = (ctypes.c_uint64 * max(cap, 1))()
+        n = ctypes.c_uint64(0)
+        rc = self.lib.npow_sweep(_root(root), threshold & M64, start & M64, count, device_mask,
+                                 cancel.address if cancel else None, ctypes.addressof(out), cap,
+                                 ctypes.byref(n))
+        _check(rc, self.lib, ok=(NPOW_OK, NPOW_CANCELLED))
+        return list(out[: min(n.value, cap)])
+
+    def values(self, root: bytes, start: int, count: int, device: int = 0) -> List[int]:
+        out = (ctypes.c_uint64 * max(count, 1))()
+        _check(self.lib.npow_values(device, _root(root), start & M64, count, ctypes.addressof(out)), self.lib)
+        return list(out[:count])
+
+    def values_pairs(self, roots: Sequence[bytes], nonces: Sequence[int], device: int = 0) -> List[int]:
+        n = len(nonces)
+        rb = b"".join(_root(r) for r in roots)
+        nn = (ctypes.c_uint64 * max(n, 1))(*[x & M64 for x in nonces])
+        out = (ctypes.c_uint64 * max(n, 1))()
+        _check(self.lib.npow_values_pairs(device, rb, ctypes.addressof(nn), n, ctypes.addressof(out)), self.lib)
+        return list(out[:n])
+
+    def set_tuning(self, iters_per_launch: int = 0, poll_interval: int = 0, blocks_per_cu: int = 0) -> None:
+        _check(self.lib.npow_set_tuning(iters_per_launch, poll_interval, blocks_per_cu), self.lib)
+
+    def stats(self, device: int = 0) -> DeviceStats:
+        s = DeviceStats()
+        _check(self.lib.npow_device_stats_get(device, ctypes.byref(s)), self.lib)
+        return s
+
+    def reset_stats(self, device: int = 0) -> None:
+        _check(self.lib.npow_device_stats_reset(device), self.lib)
+
+    def version(self) -> str:
+        return self.lib.npow_version().decode()
+
+
+_engine: Optional[Engine] = None
+_engine_lock = threading.Lock()
+
+
+def engine() -> Engine:
+    """Process-wide engine (initialised on first use; raises if no GPU)."""
+    global _engine
+    with _engine_lock:
+        if _engine is None:
+            _engine = Engine()
+        return _engine
