@@ -75,7 +75,7 @@ std::mutex g_mu;
 bool g_init = false;
 std::vector<std::unique_ptr<Device>> g_devs;
 std::atomic<uint32_t> g_iters{64};      // wave iterations per launch
-std::atomic<uint32_t> g_poll{16};       // iterations between host-abort polls (power of two)
+std::atomic<uint32_t> g_poll{64};       // a wave reads the host abort word every g_poll iterations (power of two)
 std::atomic<uint32_t> g_blocks_per_cu{8};
 
 int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }
@@ -182,7 +182,7 @@ int device_search(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_
   if (rc) return rc;
 
   LaunchArgs a{};
-  a.pre = pre;
+  fill_uniforms(a, pre);
   a.threshold = threshold;
   a.poll_mask = poll_mask();
   a.cap = 0;
@@ -309,7 +309,7 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
   int rc = reset_task(d);
   if (rc) return rc;
   LaunchArgs a{};
-  a.pre = pre;
+  fill_uniforms(a, pre);
   a.threshold = threshold;
   a.poll_mask = poll_mask();
   a.cap = (uint32_t)kHitCap;
@@ -594,7 +594,7 @@ int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t cou
   int rc = reset_task(d);
   if (rc) return rc;
   LaunchArgs a{};
-  a.pre = host_precompute(root);
+  fill_uniforms(a, host_precompute(root));
   a.poll_mask = 0;
   for (uint64_t off = 0; off < count; off += kValuesChunk) {
     const uint64_t cnt = std::min(kValuesChunk, count - off);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "npow_blake2b.h"
+#include "npow_hash_asm.inc"
 
 namespace npow {
 
@@ -12,10 +13,10 @@ constexpr int kBlock = 256;  // lanes per workgroup (4 waves of 64)
 enum class Mode : int { kSearch = 0, kSweep = 1, kValues = 2 };
 
 // Kernel arguments, passed by value: the kernarg segment lands in SGPRs, so the
-// root words, the round-1 constants and the threshold cost no memory traffic
-// per nonce (SURVEY.md §7 "Uniform data in SGPRs").
+// root-derived uniforms and the threshold cost no memory traffic per nonce
+// (SURVEY.md §7 "Uniform data in SGPRs").
 struct LaunchArgs {
-  RootPrecomp pre;     // 128 B: root words + nonce-independent round-1 state
+  uint64_t u[NPOW_ASM_N_UNIFORMS];  // nonce-independent intermediates (npow_asm_uniforms)
   uint64_t threshold;  // valid iff value >= threshold
   uint64_t base;       // first nonce of this launch (wraps mod 2^64)
   uint64_t count;      // nonces in this launch (lane index i < count)
@@ -25,11 +26,20 @@ struct LaunchArgs {
 
 // Device-resident per-task state (hipMalloc; reset by hipMemsetAsync per task).
 struct DevState {
-  uint32_t found;           // first-win slot: 0 -> 1 by atomicCAS (search)
+  union {
+    struct {
+      uint32_t found;       // first-win slot: 0 -> 1 by atomicCAS (search)
+      uint32_t abort;       // host abort relayed by the wave that saw it
+    };
+    uint64_t stop;          // both, read by every wave with one 8-byte load
+  };
   uint32_t n_hits;          // sweep: hits appended (may exceed cap)
+  uint32_t pad0;
   uint64_t nonce;           // winning nonce (search)
   uint64_t value;           // winning value (search)
   unsigned long long done;  // nonces hashed (all launches of the task)
+  uint32_t zero;            // always 0: the non-polling iterations' load target
+  uint32_t pad;
 };
 
 // Host-coherent pinned mailbox (hipHostMalloc coherent + mapped).  The winning
@@ -49,6 +59,9 @@ struct alignas(64) HostMailbox {
 // Launchers (defined in npow_kernel.hip).
 hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs& a, DevState* st,
                        HostMailbox* mb, uint64_t* out);
+// Fill a.u[] for one root (host).
+inline void fill_uniforms(LaunchArgs& a, const RootPrecomp& pre) { npow_asm_uniforms(pre.m, a.u); }
+
 hipError_t launch_pairs(int grid, hipStream_t stream, const uint64_t* roots_words, const uint64_t* nonces,
                         uint32_t n, uint64_t* out);
 

@@ -4,18 +4,18 @@
 // reference work server (client/bin/windows/nano-work-server.exe @1657474..1661900).
 // Written from the BLAKE2b definition for the gfx950 VALU, not translated:
 //
-//  * One nonce per lane, the 16-word state in VGPRs, rounds fully unrolled with
-//    the message schedule resolved at compile time: 11 of the 16 message words
-//    are zero, so their adds vanish; m1..m4 (the root) are uniform kernel
-//    arguments held in SGPRs.
+//  * The per-nonce hash is the generated instruction stream npow_hash_asm.inc
+//    (tools/gen_hash_asm.py): one nonce per lane, the 16-word state in a fixed
+//    VGPR window, 12 rounds unrolled with the message schedule resolved at
+//    generation time (11 of 16 message words are zero).  Every nonce-independent
+//    intermediate (round 1's three column steps and more) is computed once per
+//    root on the host and arrives in SGPRs.  Round 12's dead half is removed.
 //  * 64-bit adds are single `v_lshl_add_u64` instructions (measured: one
 //    64-bit add per 4.4 SIMD cycles, the cost of ONE v_add_co_u32, half the
 //    v_add_co/v_addc pair -- profiles/r01_valu_ubench.json).
-//  * Rotations are split into 32-bit halves: rotr32 is a free register swap,
-//    rotr24 / rotr16 / rotr63 are two `v_alignbit_b32` each.
-//  * Round 1's three nonce-independent column steps are precomputed per root
-//    on the host (RootPrecomp) and arrive in SGPRs.  Dead work of round 12
-//    (only v0 and v8 feed the digest word) is removed by the compiler.
+//  * Rotations are split into 32-bit halves: rotr32 is a free register swap
+//    folded into the xor that feeds it, rotr24 / rotr16 / rotr63 are two
+//    `v_alignbit_b32` each.
 //  * Grid-stride loop over the launch's nonce range; the hit test is a wave
 //    ballot, so a wave leaves the fast path only when one of its 64 lanes wins.
 //  * Search mode: first win by atomicCAS on a device slot, published to a
@@ -92,23 +92,6 @@ __device__ __forceinline__ void rounds_from(uint64_t (&v)[16], uint64_t n, const
   }
 }
 
-// Work value with round 1's nonce-independent columns taken from `col` (uniform).
-__device__ __forceinline__ uint64_t work_value_pre(uint64_t nonce, const uint64_t (&m)[4],
-                                                   const uint64_t (&col)[12]) {
-  uint64_t v[16];
-  v[0] = kH0;
-  v[4] = kIV4;
-  v[8] = kIV0;
-  v[12] = kV12;
-  G<0, 1>(v[0], v[4], v[8], v[12], nonce, m);  // round-1 column 0: the only nonce-dependent one
-  v[1] = col[0]; v[5] = col[1]; v[9] = col[2];  v[13] = col[3];
-  v[2] = col[4]; v[6] = col[5]; v[10] = col[6]; v[14] = col[7];
-  v[3] = col[8]; v[7] = col[9]; v[11] = col[10]; v[15] = col[11];
-  diagonals<0>(v, nonce, m);
-  rounds_from<1>(v, nonce, m);
-  return kH0 ^ v[0] ^ v[8];
-}
-
 // Generic work value (per-lane root): all 12 rounds on the GPU.
 __device__ __forceinline__ uint64_t work_value_full(uint64_t nonce, const uint64_t (&m)[4]) {
   uint64_t v[16] = {kH0, kIV1, kIV2, kIV3, kIV4, kIV5, kIV6, kIV7,
@@ -128,33 +111,40 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
                                                              HostMailbox* __restrict__ mb,
                                                              uint64_t* __restrict__ out) {
   // Uniform copies (the compiler keeps kernel arguments in SGPRs).
-  uint64_t m[4], col[12];
+  uint64_t u[NPOW_ASM_N_UNIFORMS];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) m[i] = a.pre.m[i];
-#pragma unroll
-  for (int i = 0; i < 12; ++i) col[i] = a.pre.col[i];
+  for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) u[i] = a.u[i];
 
   const uint32_t lane = threadIdx.x & 63;
   // First lane index of this wave; wave-uniform.
   const uint64_t wave0 =
       (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kBlock + (threadIdx.x & ~63u));
   const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  const uint32_t wave_id = (uint32_t)(wave0 >> 6);
   uint64_t done = 0;  // nonces this wave hashed (wave-uniform)
   uint32_t iter = 0;
 
   for (uint64_t ib = wave0; ib < a.count; ib += stride, ++iter) {
-    // Issue the early-exit polls first; their latency hides under the hash.
-    uint32_t stop = 0;
-    if constexpr (MODE == Mode::kSearch)
-      stop = __hip_atomic_load(&st->found, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // Early-exit polls, issued first so their latency hides under the hash:
+    //  * every iteration, one agent-scope (L2) load of the device stop word
+    //    {found, abort} -- set by a winning wave or relayed from the host;
+    //  * the host abort word lives in pinned host memory (a PCIe read), so only
+    //    one wave in poll_mask+1 reads it per iteration (staggered by wave id)
+    //    and relays a raised abort into the device stop word.
+    //  On iterations where this wave does not poll the host, the same load
+    //  reads an always-zero device word instead, so no branch forces an early
+    //  wait on it.
+    uint64_t stop_word = 0;
+    uint32_t host_abort = 0;
     if constexpr (MODE != Mode::kValues) {
-      if ((iter & a.poll_mask) == 0)
-        stop |= __hip_atomic_load(&mb->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      stop_word = __hip_atomic_load(&st->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t* poll = ((iter + wave_id) & a.poll_mask) == 0 ? &mb->abort : &st->zero;
+      host_abort = __hip_atomic_load(poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 
     const uint64_t i = ib + lane;
     const uint64_t nonce = a.base + i;
-    const uint64_t value = work_value_pre(nonce, m, col);
+    const uint64_t value = npow_asm_work_value(nonce, u);
     const bool in_range = i < a.count;
     const uint64_t rem = a.count - ib;
     done += rem < 64 ? rem : 64;
@@ -185,7 +175,11 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
           }
         }
       }
-      if (__builtin_amdgcn_readfirstlane(stop)) break;
+      if (__builtin_amdgcn_readfirstlane(host_abort)) {
+        if (lane == 0) __hip_atomic_store(&st->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+      if (__builtin_amdgcn_readfirstlane((uint32_t)stop_word | (uint32_t)(stop_word >> 32))) break;
     }
   }
   if (lane == 0 && done) atomicAdd(&st->done, (unsigned long long)done);

@@ -1,0 +1,685 @@
+#!/usr/bin/env python3
+"""Generate the gfx950 instruction stream of the Nano work hash.
+
+Writes ``nano-dpow_amd/csrc/npow_hash_asm.inc``: one inline-asm block that
+computes ``value = BLAKE2b-64(LE64(nonce) || root)`` for one nonce per lane,
+plus the host function that precomputes every nonce-independent (uniform)
+intermediate of it.
+
+Why generate instead of letting hipcc compile the C++ rounds
+(npow_kernel.hip's ``work_value_pre``): on gfx950 a 64-bit add is ONE
+``v_lshl_add_u64`` (4.4 SIMD cycles, measured in profiles/r01_valu_ubench.json)
+but it needs its operands in even-aligned VGPR pairs, while the rotations
+produce 32-bit halves (``v_alignbit_b32``).  hipcc's register allocator
+reconciles the two with ~330 ``v_mov_b32`` copies per hash and a 233-VGPR
+schedule (occupancy 2).  Here the data flow is small and fixed (96 G
+functions), so we do the instruction selection, dead-code elimination,
+scheduling and register allocation ourselves:
+
+* symbolic evaluation of the 12 rounds: m0 = nonce (per lane), m1..m4 = root
+  (uniform), m5..m15 = 0; every node that does not depend on the nonce is
+  uniform and moves to the host (``npow_asm_uniforms``) -- this subsumes the
+  round-1 column precomputation; only the uniforms the per-lane code reads
+  are passed in (as 64-bit SGPR-pair operands);
+* dead-code elimination from the single output ``H0 ^ v0 ^ v8`` (round 12's
+  unused half disappears);
+* instruction selection: add64 -> ``v_lshl_add_u64 d, a, 0, b``;
+  rotr32(x ^ y) -> two ``v_xor_b32`` writing swapped halves (the rotation is
+  free); rotr{24,16,63}(x ^ y) -> two ``v_xor_b32`` + two ``v_alignbit_b32``;
+  xor with a compile-time constant uses a 32-bit literal;
+* list scheduling by critical path with a simple latency model;
+* linear-scan register allocation at 32-bit granularity with even-aligned
+  pairs for 64-bit operands, inside a fixed VGPR window the asm statement
+  declares clobbered.
+
+Usage: python3 tools/gen_hash_asm.py [--sched rr|cp|seq] [--base 8] [--check]
+``--check`` evaluates the generated instruction stream with a tiny Python
+interpreter against hashlib on random inputs before writing the file.
+"""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import os
+import random
+import sys
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Tuple
+
+M64 = (1 << 64) - 1
+M32 = (1 << 32) - 1
+
+IV = [0x6a09e667f3bcc908, 0xbb67ae8584caa73b, 0x3c6ef372fe94f82b, 0xa54ff53a5f1d36f1,
+      0x510e527fade682d1, 0x9b05688c2b3e6c1f, 0x1f83d9abfb41bd6b, 0x5be0cd19137e2179]
+H0 = IV[0] ^ 0x01010008
+SIGMA = [
+    [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15],
+    [14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3],
+    [11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4],
+    [7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8],
+    [9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13],
+    [2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9],
+    [12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11],
+    [13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10],
+    [6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5],
+    [10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0],
+    [0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15],
+    [14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3],
+]
+
+
+def rotr(x: int, n: int) -> int:
+    return ((x >> n) | (x << (64 - n))) & M64
+
+
+# ---------------------------------------------------------------------------------------
+# Symbolic DAG
+# kinds: 'nonce', 'root'(i), 'const'(c), 'add'(a,b), 'xor'(a,b), 'rotr'(a,n)
+@dataclass(eq=False)
+class Node:
+    kind: str
+    args: tuple = ()
+    val: int = 0          # for const
+    idx: int = 0          # for root / rotation amount
+    uniform: bool = False
+    id: int = -1
+    g: int = -1           # G-function ordinal (for scheduling tie-breaks)
+
+
+class Dag:
+    def __init__(self) -> None:
+        self.nodes: List[Node] = []
+        self.cur_g = -1
+
+    def _new(self, n: Node) -> Node:
+        n.id = len(self.nodes)
+        n.g = self.cur_g
+        self.nodes.append(n)
+        return n
+
+    def nonce(self) -> Node:
+        return self._new(Node("nonce"))
+
+    def root(self, i: int) -> Node:
+        return self._new(Node("root", idx=i, uniform=True))
+
+    def const(self, c: int) -> Node:
+        return self._new(Node("const", val=c & M64, uniform=True))
+
+    def add(self, a: Node, b: Node) -> Node:
+        if a.kind == "const" and b.kind == "const":
+            return self.const(a.val + b.val)
+        if a.kind == "const" and a.val == 0:
+            return b
+        if b.kind == "const" and b.val == 0:
+            return a
+        return self._new(Node("add", (a, b), uniform=a.uniform and b.uniform))
+
+    def xor(self, a: Node, b: Node) -> Node:
+        if a.kind == "const" and b.kind == "const":
+            return self.const(a.val ^ b.val)
+        return self._new(Node("xor", (a, b), uniform=a.uniform and b.uniform))
+
+    def rotr(self, a: Node, n: int) -> Node:
+        if a.kind == "const":
+            return self.const(rotr(a.val, n))
+        return self._new(Node("rotr", (a,), idx=n, uniform=a.uniform))
+
+
+def build_hash_dag() -> Tuple[Dag, Node]:
+    d = Dag()
+    zero = d.const(0)
+    nonce = d.nonce()
+    m = [nonce] + [d.root(i) for i in range(4)] + [zero] * 11
+    v = [d.const(x) for x in [H0] + IV[1:8] + IV[0:4] + [IV[4] ^ 40, IV[5], (~IV[6]) & M64, IV[7]]]
+    gcount = 0
+
+    def G(a, b, c, dd, x, y):
+        nonlocal gcount
+        d.cur_g = gcount
+        gcount += 1
+        v[a] = d.add(d.add(v[a], m[x]), v[b])
+        v[dd] = d.rotr(d.xor(v[dd], v[a]), 32)
+        v[c] = d.add(v[c], v[dd])
+        v[b] = d.rotr(d.xor(v[b], v[c]), 24)
+        v[a] = d.add(d.add(v[a], m[y]), v[b])
+        v[dd] = d.rotr(d.xor(v[dd], v[a]), 16)
+        v[c] = d.add(v[c], v[dd])
+        v[b] = d.rotr(d.xor(v[b], v[c]), 63)
+
+    for r in range(12):
+        s = SIGMA[r]
+        G(0, 4, 8, 12, s[0], s[1])
+        G(1, 5, 9, 13, s[2], s[3])
+        G(2, 6, 10, 14, s[4], s[5])
+        G(3, 7, 11, 15, s[6], s[7])
+        G(0, 5, 10, 15, s[8], s[9])
+        G(1, 6, 11, 12, s[10], s[11])
+        G(2, 7, 8, 13, s[12], s[13])
+        G(3, 4, 9, 14, s[14], s[15])
+    d.cur_g = gcount
+    out = d.xor(d.xor(v[0], v[8]), d.const(H0))
+    return d, out
+
+
+def eval_node(n: Node, nonce: int, root_words: List[int], memo: Dict[int, int]) -> int:
+    if n.id in memo:
+        return memo[n.id]
+    k = n.kind
+    if k == "nonce":
+        r = nonce
+    elif k == "root":
+        r = root_words[n.idx]
+    elif k == "const":
+        r = n.val
+    elif k == "add":
+        r = (eval_node(n.args[0], nonce, root_words, memo) + eval_node(n.args[1], nonce, root_words, memo)) & M64
+    elif k == "xor":
+        r = eval_node(n.args[0], nonce, root_words, memo) ^ eval_node(n.args[1], nonce, root_words, memo)
+    elif k == "rotr":
+        r = rotr(eval_node(n.args[0], nonce, root_words, memo), n.idx)
+    else:
+        raise ValueError(k)
+    memo[n.id] = r
+    return r
+
+
+# ---------------------------------------------------------------------------------------
+# Lowering to "ops": each op is a small fixed instruction pattern on 64-bit values.
+@dataclass(eq=False)
+class Op:
+    kind: str               # 'add', 'xrot32', 'xrot', 'xor' (final / plain)
+    dst: Node
+    srcs: List[Node]        # lane-varying or uniform or const operands
+    n: int = 0              # rotation amount
+    id: int = -1
+    g: int = -1
+    users: List["Op"] = field(default_factory=list)
+    preds: List["Op"] = field(default_factory=list)
+    prio: float = 0.0
+
+
+def lower(dag: Dag, out: Node):
+    """Return (ops in topological order, list of uniform frontier nodes)."""
+    # collect live (reachable) lane-varying nodes
+    live: Dict[int, Node] = {}
+    stack = [out]
+    while stack:
+        n = stack.pop()
+        if n.id in live or n.uniform:
+            continue
+        live[n.id] = n
+        stack.extend(n.args)
+    # use counts of xor nodes: an xor feeding only a rotr is fused into it
+    users: Dict[int, List[Node]] = {}
+    for n in live.values():
+        for a in n.args:
+            users.setdefault(a.id, []).append(n)
+    ops: List[Op] = []
+    produced: Dict[int, Op] = {}
+    frontier: Dict[int, Node] = {}
+
+    def operand(a: Node, pair: bool = False) -> Node:
+        # 64-bit add operands that are uniform (constants included: VOP3 takes no
+        # 64-bit literal) come from SGPR pairs; xor takes 32-bit literals directly.
+        if a.uniform and (pair or a.kind != "const"):
+            frontier[a.id] = a
+        return a
+
+    for nid in sorted(live):
+        n = live[nid]
+        if n.kind == "nonce":
+            continue
+        if n.kind == "add":
+            op = Op("add", n, [operand(n.args[0], True), operand(n.args[1], True)], g=n.g)
+        elif n.kind == "rotr":
+            x = n.args[0]
+            if x.kind == "xor" and not x.uniform and len(users.get(x.id, [])) == 1:
+                kind = "xrot32" if n.idx == 32 else "xrot"
+                op = Op(kind, n, [operand(x.args[0]), operand(x.args[1])], n=n.idx, g=n.g)
+            else:
+                raise NotImplementedError("rotation of a non-xor value")
+        elif n.kind == "xor":
+            us = users.get(n.id, [])
+            if us and all(u.kind == "rotr" for u in us) and len(us) == 1:
+                continue  # fused into its rotation
+            op = Op("xor", n, [operand(n.args[0]), operand(n.args[1])], g=n.g)
+        else:
+            raise ValueError(n.kind)
+        op.id = len(ops)
+        ops.append(op)
+        produced[n.id] = op
+    # dependency edges
+    for op in ops:
+        for s in op.srcs:
+            p = produced.get(s.id)
+            if p is not None:
+                op.preds.append(p)
+                p.users.append(op)
+    return ops, list(frontier.values()), produced
+
+
+# issue cost (SIMD cycles per wave64 instruction, profiles/r01_valu_ubench.json) and latency model
+COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b32": 4.3, "v_lshl_add_u64": 4.4}
+LAT = 8.0
+
+
+def op_cost(op: Op) -> float:
+    def xc(s):
+        if s.kind == "const":
+            return COST["v_xor_b32_k"]
+        if s.uniform:
+            return COST["v_xor_b32_s"]
+        return COST["v_xor_b32"]
+    if op.kind == "add":
+        return COST["v_lshl_add_u64"]
+    x = 2 * max(xc(op.srcs[0]), xc(op.srcs[1]))
+    if op.kind == "xrot":
+        return x + 2 * COST["v_alignbit_b32"]
+    return x
+
+
+def schedule(ops: List[Op], mode: str) -> List[Op]:
+    # priority = longest path (in cost) to the end
+    for op in reversed(ops):
+        op.prio = op_cost(op) + LAT + max((u.prio for u in op.users), default=0.0)
+    if mode == "seq":
+        return list(ops)
+    n_pred = {op.id: len(op.preds) for op in ops}
+    ready_at = {op.id: 0.0 for op in ops}
+    ready = [op for op in ops if not op.preds]
+    t = 0.0
+    order: List[Op] = []
+    last_g = -1
+    while ready:
+        avail = [op for op in ready if ready_at[op.id] <= t]
+        pool = avail if avail else ready
+        if mode == "cp":
+            best = max(pool, key=lambda o: (o.prio, -o.id))
+        elif mode == "rr":
+            # round-robin over G functions among available ops, preferring a different G than last
+            cand = [o for o in pool if o.g != last_g] or pool
+            best = max(cand, key=lambda o: (o.prio, -o.id))
+        else:
+            raise ValueError(mode)
+        ready.remove(best)
+        if not avail:
+            t = ready_at[best.id]
+        t += op_cost(best)
+        last_g = best.g
+        order.append(best)
+        for u in best.users:
+            n_pred[u.id] -= 1
+            ready_at[u.id] = max(ready_at[u.id], t + LAT)
+            if n_pred[u.id] == 0:
+                ready.append(u)
+    assert len(order) == len(ops)
+    return order
+
+
+# ---------------------------------------------------------------------------------------
+# Register allocation + emission
+class Alloc:
+    def __init__(self, base: int, limit: int) -> None:
+        self.base, self.limit = base, limit
+        self.free = set(range(base, limit))
+        self.max_used = base
+
+    def take1(self, avoid=()) -> int:
+        for r in sorted(self.free):
+            if r not in avoid:
+                self.free.remove(r)
+                self.max_used = max(self.max_used, r + 1)
+                return r
+        raise RuntimeError("out of VGPRs")
+
+    def take2(self, avoid=()) -> int:
+        for r in sorted(self.free):
+            if r % 2 == 0 and r + 1 in self.free and r not in avoid and r + 1 not in avoid:
+                self.free.remove(r)
+                self.free.remove(r + 1)
+                self.max_used = max(self.max_used, r + 2)
+                return r
+        raise RuntimeError("out of VGPR pairs")
+
+    def release(self, r: int) -> None:
+        assert r not in self.free
+        self.free.add(r)
+
+
+def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int):
+    """Return (asm lines, uniform operand index map, max vgpr used, counts)."""
+    uni_index = {n.id: i for i, n in enumerate(frontier)}
+    # remaining-use counters per lane-varying node (64-bit), counting each op read once
+    remaining: Dict[int, int] = {}
+    for op in order:
+        for s in op.srcs:
+            if not s.uniform:
+                remaining[s.id] = remaining.get(s.id, 0) + 1
+    al = Alloc(base, limit)
+    loc: Dict[int, int] = {}  # node id -> even base register of its pair
+    NONCE = "%[nonce]"
+    lines: List[str] = []
+    counts: Dict[str, int] = {}
+
+    def cnt(k):
+        counts[k] = counts.get(k, 0) + 1
+
+    def pair(n: Node) -> str:
+        if n.kind == "nonce":
+            return NONCE
+        if n.uniform:
+            return f"%[u{uni_index[n.id]}]"
+        r = loc[n.id]
+        return f"v[{r}:{r + 1}]"
+
+    def half(n: Node, hi: int) -> str:
+        """32-bit operand text for half `hi` of n (for v_xor_b32 src0 may be literal or SGPR)."""
+        if n.kind == "const":
+            return f"0x{(n.val >> (32 * hi)) & M32:08x}"
+        if n.kind == "nonce":
+            return f"%[nonce_{'hi' if hi else 'lo'}]"
+        if n.uniform:
+            return f"%[u{uni_index[n.id]}_{'hi' if hi else 'lo'}]"
+        return f"v{loc[n.id] + hi}"
+
+    def dying(op: Op) -> List[Node]:
+        ds = []
+        seen = set()
+        for s in op.srcs:
+            if s.uniform or s.kind == "nonce" or s.id in seen:
+                continue
+            seen.add(s.id)
+            if remaining[s.id] == sum(1 for x in op.srcs if x.id == s.id):
+                ds.append(s)
+        return ds
+
+    def consume(op: Op) -> None:
+        seen = set()
+        for s in op.srcs:
+            if s.uniform or s.kind == "nonce" or s.id in seen:
+                continue
+            seen.add(s.id)
+            remaining[s.id] -= sum(1 for x in op.srcs if x.id == s.id)
+            if remaining[s.id] == 0:
+                r = loc.pop(s.id)
+                al.release(r)
+                al.release(r + 1)
+
+    def xor_operands(a: Node, b: Node, hi: int) -> Tuple[str, str]:
+        # VOP2 v_xor_b32: src0 may be VGPR/SGPR/literal, src1 must be VGPR
+        if not (a.uniform or a.kind == "nonce") or (b.kind == "const" or b.uniform):
+            a, b = b, a
+        if (a.uniform or a.kind == "const") and (b.uniform or b.kind == "const"):
+            raise RuntimeError("uniform xor uniform should have been folded")
+        # b must be in a VGPR: nonce or lane-varying
+        return half(a, hi), half(b, hi)
+
+    for op in order:
+        a, b = op.srcs
+        if op.kind == "add":
+            if a.uniform and b.uniform:
+                raise RuntimeError("uniform add should have been folded")
+            # one instruction reads both sources before writing: in place on a dying source is fine
+            ta, tb = pair(a), pair(b)
+            if a.uniform:  # VOP3 src0 may be an SGPR pair too, keep the VGPR first for readability
+                ta, tb = tb, ta
+            consume(op)
+            r = al.take2()
+            loc[op.dst.id] = r
+            lines.append(f"v_lshl_add_u64 v[{r}:{r + 1}], {ta}, 0, {tb}")
+            cnt("v_lshl_add_u64")
+        elif op.kind == "xrot32":
+            # dst.lo = a.hi ^ b.hi ; dst.hi = a.lo ^ b.lo  (rotation by 32 is the swap).
+            # dst.lo is written before the lo halves are read: keep it off them.
+            s0h, s1h = xor_operands(a, b, 1)
+            s0l, s1l = xor_operands(a, b, 0)
+            lo_regs = tuple(loc[x.id] for x in (a, b) if x.id in loc)
+            consume(op)
+            r = al.take2(avoid=lo_regs)
+            loc[op.dst.id] = r
+            lines.append(f"v_xor_b32 v{r}, {s0h}, {s1h}")
+            lines.append(f"v_xor_b32 v{r + 1}, {s0l}, {s1l}")
+            cnt("v_xor_b32")
+            cnt("v_xor_b32")
+        elif op.kind == "xrot":
+            s0l, s1l = xor_operands(a, b, 0)
+            s0h, s1h = xor_operands(a, b, 1)
+            hi_regs = tuple(loc[x.id] + 1 for x in (a, b) if x.id in loc)
+            consume(op)
+            tl = al.take1(avoid=hi_regs)   # written before the hi halves are read
+            th = al.take1(avoid=(tl,))
+            lines.append(f"v_xor_b32 v{tl}, {s0l}, {s1l}")
+            lines.append(f"v_xor_b32 v{th}, {s0h}, {s1h}")
+            r = al.take2(avoid=(tl, th))
+            loc[op.dst.id] = r
+            n = op.n
+            if n < 32:
+                lines.append(f"v_alignbit_b32 v{r}, v{th}, v{tl}, {n}")
+                lines.append(f"v_alignbit_b32 v{r + 1}, v{tl}, v{th}, {n}")
+            else:
+                k = n - 32
+                lines.append(f"v_alignbit_b32 v{r}, v{tl}, v{th}, {k}")
+                lines.append(f"v_alignbit_b32 v{r + 1}, v{th}, v{tl}, {k}")
+            al.release(tl)
+            al.release(th)
+            cnt("v_xor_b32")
+            cnt("v_xor_b32")
+            cnt("v_alignbit_b32")
+            cnt("v_alignbit_b32")
+        elif op.kind == "xor":
+            s0l, s1l = xor_operands(a, b, 0)
+            s0h, s1h = xor_operands(a, b, 1)
+            consume(op)
+            if op.dst is out:
+                lines.append(f"v_xor_b32 %[value_lo], {s0l}, {s1l}")
+                lines.append(f"v_xor_b32 %[value_hi], {s0h}, {s1h}")
+            else:
+                r = al.take2()
+                loc[op.dst.id] = r
+                lines.append(f"v_xor_b32 v{r}, {s0l}, {s1l}")
+                lines.append(f"v_xor_b32 v{r + 1}, {s0h}, {s1h}")
+            cnt("v_xor_b32")
+            cnt("v_xor_b32")
+        else:
+            raise ValueError(op.kind)
+    return lines, uni_index, al.max_used, counts
+
+
+# ---------------------------------------------------------------------------------------
+# A tiny interpreter of the emitted text, to check the generator itself against hashlib.
+def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
+    regs: Dict[int, int] = {}
+    named: Dict[str, int] = {"nonce_lo": nonce & M32, "nonce_hi": nonce >> 32}
+    for i, u in enumerate(uni_vals):
+        named[f"u{i}_lo"] = u & M32
+        named[f"u{i}_hi"] = u >> 32
+
+    def rd32(tok: str) -> int:
+        tok = tok.strip()
+        if tok.startswith("0x"):
+            return int(tok, 16)
+        if tok.startswith("%["):
+            return named[tok[2:-1]]
+        if tok.startswith("v") and tok[1:].isdigit():
+            return regs[int(tok[1:])]
+        return int(tok)
+
+    def rd64(tok: str) -> int:
+        tok = tok.strip()
+        if tok == "%[nonce]":
+            return nonce
+        if tok.startswith("%[u"):
+            return uni_vals[int(tok[3:-1])]
+        assert tok.startswith("v["), tok
+        lo, hi = tok[2:-1].split(":")
+        lo, hi = int(lo), int(hi)
+        assert hi == lo + 1 and lo % 2 == 0, tok
+        return regs[lo] | (regs[hi] << 32)
+
+    def wr32(tok: str, val: int) -> None:
+        tok = tok.strip()
+        if tok.startswith("%["):
+            named[tok[2:-1]] = val & M32
+        else:
+            regs[int(tok[1:])] = val & M32
+
+    for ln in lines:
+        opc, rest = ln.split(" ", 1)
+        ops = [t.strip() for t in rest.split(",")]
+        if opc == "v_xor_b32":
+            wr32(ops[0], rd32(ops[1]) ^ rd32(ops[2]))
+        elif opc == "v_alignbit_b32":
+            hi, lo, sh = rd32(ops[1]), rd32(ops[2]), int(ops[3])
+            wr32(ops[0], (((hi << 32) | lo) >> sh) & M32)
+        elif opc == "v_lshl_add_u64":
+            x = rd64(ops[1]) << int(ops[2])
+            y = rd64(ops[3])
+            s = (x + y) & M64
+            lo = int(ops[0][2:-1].split(":")[0])
+            regs[lo] = s & M32
+            regs[lo + 1] = s >> 32
+        else:
+            raise ValueError(opc)
+    return named["value_lo"] | (named["value_hi"] << 32)
+
+
+def uniform_values(frontier: List[Node], root_words: List[int]) -> List[int]:
+    memo: Dict[int, int] = {}
+    return [eval_node(n, 0, root_words, memo) for n in frontier]
+
+
+# ---------------------------------------------------------------------------------------
+def c_expr_program(frontier: List[Node]) -> List[str]:
+    """C statements computing every frontier uniform from m[0..3] (host side)."""
+    need: Dict[int, Node] = {}
+    stack = list(frontier)
+    while stack:
+        n = stack.pop()
+        if n.id in need or n.kind in ("const", "root"):
+            continue
+        need[n.id] = n
+        stack.extend(n.args)
+
+    def ref(n: Node) -> str:
+        if n.kind == "const":
+            return f"0x{n.val:016x}ull"
+        if n.kind == "root":
+            return f"m[{n.idx}]"
+        return f"t{n.id}"
+
+    out = []
+    for nid in sorted(need):
+        n = need[nid]
+        if n.kind == "add":
+            out.append(f"const uint64_t t{nid} = {ref(n.args[0])} + {ref(n.args[1])};")
+        elif n.kind == "xor":
+            out.append(f"const uint64_t t{nid} = {ref(n.args[0])} ^ {ref(n.args[1])};")
+        elif n.kind == "rotr":
+            k = n.idx
+            out.append(f"const uint64_t t{nid} = ({ref(n.args[0])} >> {k}) | ({ref(n.args[0])} << {64 - k});")
+        else:
+            raise ValueError(n.kind)
+    for i, n in enumerate(frontier):
+        out.append(f"u[{i}] = {ref(n)};")
+    return out
+
+
+def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List[str], vbase: int, vmax: int,
+              counts: Dict[str, int], sched: str, est_cycles: float) -> None:
+    nu = len(frontier)
+    clobbers = ", ".join(f'"v{r}"' for r in range(vbase, vmax))
+    text = "\n".join(lines)
+    ops_in = []
+    for nm, expr in [("nonce", "nonce"), ("nonce_lo", "(uint32_t)nonce"), ("nonce_hi", "(uint32_t)(nonce >> 32)")]:
+        if f"%[{nm}]" in text:
+            ops_in.append(f'[{nm}] "v"({expr})')
+    for i in range(nu):
+        if f"%[u{i}]" in text:
+            ops_in.append(f'[u{i}] "s"(u[{i}])')
+        if f"%[u{i}_lo]" in text:
+            ops_in.append(f'[u{i}_lo] "s"((uint32_t)u[{i}])')
+        if f"%[u{i}_hi]" in text:
+            ops_in.append(f'[u{i}_hi] "s"((uint32_t)(u[{i}] >> 32))')
+    uni_ops = ",\n        ".join(ops_in)
+    body = "\n".join(f'      "{ln}\\n"' for ln in lines)
+    cnt_txt = ", ".join(f"{k} {v}" for k, v in sorted(counts.items()))
+    txt = f"""// GENERATED by tools/gen_hash_asm.py (--sched {sched}) -- do not edit by hand.
+//
+// gfx950 instruction stream of the Nano work value for one nonce per lane:
+//   value = BLAKE2b-64(LE64(nonce) || root)   (nano-work-server.exe @1661643 nano_work)
+// Per nonce: {sum(counts.values())} VALU instructions ({cnt_txt});
+// VGPR window v{vbase}..v{vmax - 1}; {nu} uniform 64-bit values, {len(ops_in)} asm input operands;
+// modelled issue cost {est_cycles:.0f} SIMD cycles per wave (64 nonces).
+#pragma once
+#include <stdint.h>
+
+#define NPOW_ASM_N_UNIFORMS {nu}
+
+// Host: every nonce-independent intermediate the per-lane stream reads.
+static inline void npow_asm_uniforms(const uint64_t m[4], uint64_t u[NPOW_ASM_N_UNIFORMS]) {{
+{chr(10).join('  ' + s for s in host_prog)}
+}}
+
+__device__ __forceinline__ uint64_t npow_asm_work_value(uint64_t nonce, const uint64_t (&u)[NPOW_ASM_N_UNIFORMS]) {{
+#if defined(__HIP_DEVICE_COMPILE__)
+  uint32_t value_lo, value_hi;
+  asm(
+{body}
+      : [value_lo] "=&v"(value_lo), [value_hi] "=&v"(value_hi)
+      : {uni_ops}
+      : {clobbers});
+  return ((uint64_t)value_hi << 32) | value_lo;
+#else
+  (void)nonce; (void)u;
+  return 0;  // host compilation pass: device code is never executed here
+#endif
+}}
+"""
+    with open(path, "w") as f:
+        f.write(txt)
+
+
+def main() -> int:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--sched", default="rr", choices=["rr", "cp", "seq"])
+    ap.add_argument("--base", type=int, default=16, help="first VGPR of the clobbered window")
+    ap.add_argument("--limit", type=int, default=64, help="one past the last VGPR the window may use")
+    ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
+                                                  "nano-dpow_amd", "csrc", "npow_hash_asm.inc"))
+    ap.add_argument("--check", type=int, default=64, help="random (root, nonce) pairs to check vs hashlib")
+    args = ap.parse_args()
+
+    dag, out = build_hash_dag()
+    ops, frontier, _ = lower(dag, out)
+    order = schedule(ops, args.sched)
+    lines, _uni, vmax, counts = emit(order, frontier, out, args.base, args.limit)
+    est = 0.0
+    for ln in lines:
+        opc = ln.split(" ", 1)[0]
+        if opc == "v_xor_b32":
+            src0 = ln.split(",")[1].strip()
+            est += COST["v_xor_b32_k"] if src0.startswith("0x") else (
+                COST["v_xor_b32_s"] if src0.startswith("%[u") else COST["v_xor_b32"])
+        else:
+            est += COST[opc]
+    rng = random.Random(2024)
+    for _ in range(args.check):
+        root = bytes(rng.getrandbits(8) for _ in range(32))
+        nonce = rng.getrandbits(64)
+        words = [int.from_bytes(root[8 * i:8 * i + 8], "little") for i in range(4)]
+        uv = uniform_values(frontier, words)
+        got = interpret(lines, nonce, uv)
+        want = int.from_bytes(hashlib.blake2b(nonce.to_bytes(8, "little") + root, digest_size=8).digest(), "little")
+        if got != want:
+            print(f"MISMATCH root={root.hex()} nonce={nonce:016x} got={got:016x} want={want:016x}")
+            return 1
+    host_prog = c_expr_program(frontier)
+    write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, args.sched, est)
+    print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
+          f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
