@@ -1,0 +1,84 @@
+"""``python -m nanopow`` -- run the nano-work-server-compatible work server.
+
+Accepts the reference work server's flags (nano-work-server.exe @1681064;
+launched as ``--gpu 0:0 -l 127.0.0.1:7000`` by client/run_windows.bat:27 and
+client/README.md:31):
+
+  -l/--listen-address ADDR      default 127.0.0.1:7000 (the DPoW client's --worker_uri default)
+  -g/--gpu PLATFORM:DEVICE[:THREADS]   repeatable; PLATFORM is ignored (HIP has one)
+  -c/--cpu-threads N            rejected: this engine runs on MI355X GPUs only
+  --gpu-local-work-size N       accepted and ignored (workgroups are 256 lanes on gfx950)
+  --shuffle                     pick a random queued request instead of the oldest
+
+Without --gpu every visible GPU is used.
+"""
+from __future__ import annotations
+
+import argparse
+import logging
+import sys
+
+from . import work as W
+
+
+def parse_args(argv=None) -> argparse.Namespace:
+    ap = argparse.ArgumentParser(prog="nanopow", description="Provides a work server for Nano without a full node "
+                                 "(MI355X / gfx950 engine).")
+    ap.add_argument("-l", "--listen-address", "--listen_address", dest="listen", default="127.0.0.1:7000",
+                    metavar="ADDR", help="Specifies the address to listen on.")
+    ap.add_argument("-g", "--gpu", action="append", default=[], metavar="PLATFORM:DEVICE:THREADS",
+                    help="Specifies which GPU(s) to use. THREADS is optional and defaults to 1048576.")
+    ap.add_argument("-c", "--cpu-threads", "--cpu_threads", dest="cpu_threads", type=int, default=0,
+                    metavar="THREADS", help="Not supported: this engine runs on GPUs only.")
+    ap.add_argument("--gpu-local-work-size", "--gpu_local_work_size", dest="local_work_size", type=int,
+                    default=None, metavar="N", help="Accepted for compatibility; gfx950 workgroups are fixed.")
+    ap.add_argument("--shuffle", action="store_true",
+                    help="Pick a random request from the queue instead of the oldest.")
+    ap.add_argument("--base-difficulty", default=W.fmt_u64(W.DEFAULT_BASE),
+                    help="Threshold multipliers are quoted against (default fffffff800000000).")
+    ap.add_argument("-v", "--verbose", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    logging.basicConfig(level=logging.DEBUG if args.verbose else logging.INFO,
+                        format="%(asctime)s %(levelname)s %(message)s")
+    if args.cpu_threads:
+        print("CPU workers are not supported by this engine: use --gpu PLATFORM:DEVICE", file=sys.stderr)
+        return 2
+    try:
+        base = W.parse_threshold(args.base_difficulty)
+        gpus = [W.parse_gpu_spec(s) for s in args.gpu]
+        host, _, port = args.listen.rpartition(":")
+        host = host.strip("[]") or "127.0.0.1"
+        port_i = int(port)
+    except (W.RequestError, ValueError) as e:
+        print(f"Failed to parse options: {e}", file=sys.stderr)
+        return 2
+
+    from ._lib import engine  # loads libnanopow.so; raises if it or the GPU is missing
+    from .server import HttpWorkServer, WorkServer
+
+    eng = engine()
+    mask = 0
+    for _platform, device, _threads in gpus:
+        if device >= eng.n_devices:
+            print(f"GPU {device} not found ({eng.n_devices} visible)", file=sys.stderr)
+            return 2
+        mask |= 1 << device
+    srv = HttpWorkServer(WorkServer(eng, base_threshold=base, shuffle=args.shuffle, device_mask=mask), host, port_i)
+    logging.info("Configured for the live network with threshold %016x", base)
+    logging.info("Ready to receive requests on %s (%d GPU(s), %s)", srv.address,
+                 bin(mask).count("1") if mask else eng.n_devices, eng.version())
+    try:
+        srv.serve_forever()
+    except KeyboardInterrupt:
+        pass
+    finally:
+        srv.stop()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,76 @@
+"""The C ABI library: loads, exports every symbol include/nanopow.h declares, CPU entry points.
+
+No GPU compute here (CPU suite); tests/test_gpu_parity.py covers the kernels.
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT, load_golden
+from nanopow import _lib
+
+HEADER = os.path.join(ROOT, "include", "nanopow.h")
+
+
+def declared_symbols():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(npow_[a-z_]+)\s*\(", txt)))
+
+
+def test_library_built_in_tree():
+    assert os.path.exists(_lib.LIB_PATH), "run __graft_entry__.build() / make -C nano-dpow_amd/csrc"
+
+
+def test_exports_every_declared_symbol():
+    syms = declared_symbols()
+    assert len(syms) >= 13
+    assert sorted(syms) == sorted(_lib.EXPORTED_SYMBOLS)
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r" T (npow_\w+)$", out, flags=re.M))
+    missing = set(syms) - exported
+    assert not missing, missing
+    lib = _lib.load()
+    for s in syms:
+        assert hasattr(lib, s)
+
+
+def test_gfx950_code_object_embedded():
+    # the fat binary carries an amdgcn-amd-amdhsa--gfx950 code object (no other target)
+    blob = open(_lib.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert not re.search(rb"amdgcn-amd-amdhsa--gfx9[0-4]\d", blob)
+
+
+def test_cpu_work_value_matches_golden():
+    lib = _lib.load()
+    g = load_golden("work_values.json")["triples"]
+    for r, n, v in g:
+        assert lib.npow_work_value(bytes.fromhex(r), int(n, 16)) == int(v, 16)
+
+
+def test_version_string():
+    assert b"gfx950" in _lib.load().npow_version()
+
+
+def test_uninitialised_calls_fail_cleanly():
+    lib = _lib.load()
+    out = ctypes.c_uint64(0)
+    # search before npow_init (or without a GPU) must return an error, never fall back to the CPU
+    rc = lib.npow_search(b"\x00" * 32, 0, 0, 0, 0, None, ctypes.byref(out), None, None)
+    assert rc < 0
+    assert lib.npow_last_error()
+
+
+def test_init_without_gpu_reports_no_device():
+    import torch  # noqa: F401  (only to ask whether this host has a GPU)
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    n = ctypes.c_int(-1)
+    rc = _lib.load().npow_init(ctypes.byref(n))
+    assert rc == _lib.NPOW_ERR_NO_DEVICE
+    with pytest.raises(_lib.NanoPowError):
+        _lib.Engine()

@@ -1,0 +1,171 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bit-exact throughout (integer work).  Run on an MI355X: ``pytest -m gpu``.
+Covers: every golden (root, nonce, value) triple through both GPU code paths
+(specialised per-root stream npow_values, generic per-lane npow_values_pairs);
+contiguous value ranges incl. 2^32 and 2^64 carries; every exhaustive sweep
+fixture (8 roots x [0, 2^28), hashlib ranges, the range across 2^64 -> 0) and,
+at BASELINE config 3's full size, the 2^36 sweep; first-win search validity
+at the BASELINE thresholds; threshold edges; exhaustion, cancellation,
+empty / ragged ranges; multi-device masks.
+"""
+import os
+import random
+import threading
+import time
+
+import pytest
+
+import oracle
+from conftest import load_golden
+from nanopow import _lib
+
+pytestmark = pytest.mark.gpu
+M64 = (1 << 64) - 1
+SEND, RECEIVE, LOW = 0xfffffff800000000, 0xfffffe0000000000, 0xfffff00000000000
+
+
+def test_native_library_is_the_hip_path(gpu_engine):
+    assert "gfx950" in gpu_engine.version()
+    st = gpu_engine.stats(0)
+    assert st.cus >= 1 and st.grid >= st.cus
+
+
+def test_golden_triples_both_gpu_paths(gpu_engine):
+    g = load_golden("work_values.json")["triples"]
+    roots = [bytes.fromhex(r) for r, _, _ in g]
+    nonces = [int(n, 16) for _, n, _ in g]
+    want = [int(v, 16) for _, _, v in g]
+    assert gpu_engine.values_pairs(roots, nonces) == want
+    got = [gpu_engine.values(r, n, 1)[0] for r, n in zip(roots[:512], nonces[:512])]
+    assert got == want[:512]
+
+
+@pytest.mark.parametrize("start,count", [
+    (0, 1 << 16), (0xffffffff - 1000, 5000), ((1 << 64) - 3000, 6000), (12345, 1), (7, 65), (99, 64 * 1000 + 17)])
+def test_value_ranges_vs_oracle(gpu_engine, start, count):
+    rng = random.Random(start ^ count)
+    root = bytes(rng.getrandbits(8) for _ in range(32))
+    got = gpu_engine.values(root, start, count)
+    roots = [root] * count
+    want = oracle.work_values(roots, [(start + i) & M64 for i in range(count)])
+    assert got == want
+
+
+def test_sweep_fixtures(gpu_engine):
+    for c in load_golden("sweeps_small.json")["cases"]:
+        got = gpu_engine.sweep(bytes.fromhex(c["root"]), int(c["threshold"], 16), int(c["start"], 16), c["count"])
+        assert [f"{h:016x}" for h in got] == c["hits"], c["method"]
+
+
+def test_sweep_2p36_full_size(gpu_engine):
+    """BASELINE config 3: exhaustive 2^36 sweep, bit-exact hit set vs the CPU fixture."""
+    path = os.path.join(os.path.dirname(__file__), "golden", "sweep_2p36.json")
+    if not os.path.exists(path):
+        pytest.skip("sweep_2p36.json not generated")
+    g = load_golden("sweep_2p36.json")
+    t = time.time()
+    got = gpu_engine.sweep(bytes.fromhex(g["root"]), int(g["threshold"], 16), 0, g["count"], cap=1 << 12)
+    dt = time.time() - t
+    assert [f"{h:016x}" for h in got] == g["hits"]
+    print(f"2^36 sweep: {len(got)} hits in {dt:.2f} s = {(1 << 36) / dt / 1e9:.2f} Gnonce/s")
+
+
+def test_sweep_edges(gpu_engine):
+    root = bytes(range(32))
+    assert gpu_engine.sweep(root, 0, 5, 0) == []
+    # threshold 0: every nonce is a hit (exact count, order, ragged length)
+    got = gpu_engine.sweep(root, 0, 100, 1000, cap=2000)
+    assert got == list(range(100, 1100))
+    got = gpu_engine.sweep(root, 0, M64 - 9, 20, cap=100)  # wraps 2^64 -> 0
+    assert got == [(M64 - 9 + i) & M64 for i in range(20)]
+    # threshold = an exact value: the nonce with that value is a hit (>=), value+1 excludes it
+    vals = gpu_engine.values(root, 0, 4096)
+    top = max(range(4096), key=lambda i: vals[i])
+    assert gpu_engine.sweep(root, vals[top], 0, 4096) == [top]
+    assert gpu_engine.sweep(root, vals[top] + 1, 0, 4096) == []
+
+
+def test_sweep_capacity_error(gpu_engine):
+    with pytest.raises(_lib.NanoPowError) as ei:
+        gpu_engine.sweep(bytes(32), 0, 0, 5000, cap=100)
+    assert ei.value.code == _lib.NPOW_ERR_CAPACITY
+
+
+@pytest.mark.parametrize("thr", [LOW, RECEIVE, SEND])
+def test_search_results_revalidate(gpu_engine, thr):
+    rng = random.Random(thr)
+    n = 40 if thr != SEND else 12
+    for _ in range(n):
+        root = bytes(rng.getrandbits(8) for _ in range(32))
+        r = gpu_engine.search(root, thr, start=rng.getrandbits(64))
+        assert r.status == _lib.NPOW_OK
+        assert oracle.work_value_hashlib(root, r.nonce) == r.value >= thr
+        assert r.nonces_done > 0
+
+
+def test_search_is_first_in_small_ranges(gpu_engine):
+    """With one launch covering [start, start+count) the winner must be a real hit of that
+    range (any of them: lanes race), and exhaustion must be reported when there is none."""
+    c = load_golden("sweeps_small.json")["cases"][1]  # RECEIVE hits of root 0 in [0, 2^28)
+    root, thr = bytes.fromhex(c["root"]), int(c["threshold"], 16)
+    hits = [int(h, 16) for h in c["hits"]]
+    r = gpu_engine.search(root, thr, start=0, max_nonces_per_device=1 << 28)
+    assert r.status == _lib.NPOW_OK and r.nonce in hits
+    # a range with no hit: between two consecutive hits
+    a, b = hits[0], hits[1]
+    r = gpu_engine.search(root, thr, start=a + 1, max_nonces_per_device=b - a - 1)
+    assert r.status == _lib.NPOW_EXHAUSTED and r.nonce is None
+    assert r.nonces_done == b - a - 1
+
+
+def test_search_threshold_edges(gpu_engine):
+    root = bytes(32)
+    r = gpu_engine.search(root, 0, start=42)
+    assert r.status == _lib.NPOW_OK and r.value == oracle.work_value(root, r.nonce)
+    r = gpu_engine.search(root, M64, start=0, max_nonces_per_device=1 << 22)
+    assert r.status == _lib.NPOW_EXHAUSTED
+
+
+def test_search_cancel_from_another_thread(gpu_engine):
+    tok = _lib.CancelToken()
+    out = {}
+    th = threading.Thread(target=lambda: out.setdefault("r", gpu_engine.search(bytes(32), M64, cancel=tok)))
+    t0 = time.time()
+    th.start()
+    time.sleep(0.2)
+    tok.set()
+    th.join(10)
+    assert not th.is_alive()
+    assert out["r"].status == _lib.NPOW_CANCELLED
+    assert out["r"].nonces_done > 0
+    assert time.time() - t0 < 5
+
+
+def test_device_masks(gpu_engine):
+    root = bytes(range(1, 33))
+    n = gpu_engine.n_devices
+    r = gpu_engine.search(root, RECEIVE, device_mask=(1 << n) - 1)
+    assert r.status == _lib.NPOW_OK and oracle.work_value(root, r.nonce) >= RECEIVE
+    with pytest.raises(_lib.NanoPowError):
+        gpu_engine.search(root, RECEIVE, device_mask=1 << 40)
+
+
+def test_search_batch(gpu_engine):
+    rng = random.Random(5)
+    roots = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(16)]
+    thr = [RECEIVE] * 15 + [M64]
+    toks = [None] * 15 + [_lib.CancelToken()]
+    toks[15].set()
+    res, done = gpu_engine.search_batch(roots, thr, cancels=toks)
+    for root, r in zip(roots[:15], res[:15]):
+        assert r.status == _lib.NPOW_OK and oracle.work_value(root, r.nonce) == r.value >= RECEIVE
+    assert res[15].status == _lib.NPOW_CANCELLED
+    assert done > 0
+
+
+def test_stats_count_every_nonce(gpu_engine):
+    gpu_engine.reset_stats(0)
+    gpu_engine.sweep(bytes(32), SEND, 0, 10_000_019)
+    st = gpu_engine.stats(0)
+    assert st.nonces == 10_000_019 and st.launches >= 1 and st.kernel_ms > 0

@@ -1,0 +1,61 @@
+"""End to end on the GPU: the WorkHandler transcript against the work server backed by libnanopow."""
+import json
+import threading
+import time
+import urllib.request
+
+import pytest
+
+import oracle
+from conftest import load_golden
+from nanopow.server import HttpWorkServer, WorkServer
+
+pytestmark = pytest.mark.gpu
+
+
+def post(addr, obj, timeout=60):
+    req = urllib.request.Request(f"http://{addr}", data=json.dumps(obj).encode(), method="POST",
+                                 headers={"Content-Type": "application/json"})
+    with urllib.request.urlopen(req, timeout=timeout) as r:
+        return json.loads(r.read())
+
+
+@pytest.fixture()
+def gpu_server(gpu_engine):
+    srv = HttpWorkServer(WorkServer(gpu_engine), "127.0.0.1", 0).start()
+    yield srv
+    srv.stop()
+
+
+def test_transcript_on_gpu(gpu_server):
+    t = load_golden("workhandler_transcript.json")
+    reqs = t["requests"]
+    assert "error" in post(gpu_server.address, reqs[0])
+    r = post(gpu_server.address, reqs[1])
+    root, thr = bytes.fromhex(reqs[1]["hash"]), int(reqs[1]["difficulty"], 16)
+    assert oracle.work_value_hashlib(root, int(r["work"], 16)) == int(r["difficulty"], 16) >= thr
+    hold = dict(reqs[2], difficulty="ffffffffffffffff")
+    box = {}
+    th = threading.Thread(target=lambda: box.setdefault("r", post(gpu_server.address, hold)))
+    th.start()
+    time.sleep(0.5)
+    t0 = time.time()
+    assert post(gpu_server.address, reqs[3]) == {}
+    th.join(10)
+    assert box["r"] == {"error": "Cancelled"}
+    assert time.time() - t0 < 2.0
+
+
+def test_send_difficulty_generate_and_validate(gpu_server):
+    for i in range(5):
+        h = f"{i + 1:064X}"
+        r = post(gpu_server.address, {"action": "work_generate", "hash": h, "difficulty": "fffffff800000000"})
+        v = oracle.work_value_hashlib(bytes.fromhex(h), int(r["work"], 16))
+        assert v >= 0xfffffff800000000 and r["difficulty"] == f"{v:016x}"
+        chk = post(gpu_server.address, {"action": "work_validate", "hash": h, "work": r["work"]})
+        assert chk["valid_all"] == "1" and chk["valid_receive"] == "1"
+
+
+def test_benchmark_on_gpu(gpu_server):
+    r = post(gpu_server.address, {"action": "benchmark", "count": 10})
+    assert r["count"] == "10" and int(r["duration"]) > 0

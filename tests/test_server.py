@@ -1,0 +1,201 @@
+"""Work-server JSON surface over real HTTP (CPU; the engine is the oracle stand-in).
+
+The contract is the DPoW client's WorkHandler (client/work_handler.py), captured
+in tests/golden/workhandler_transcript.json by gen_transcript.py: probe with an
+unknown action and read ['error'] (:53); serial work_generate and read ['work']
+(:104-117); work_cancel on a second connection while a generate is pending,
+which must then answer {"error": "Cancelled"} (:61-80, :109-114).
+"""
+import json
+import threading
+import time
+import urllib.request
+
+import pytest
+
+import oracle
+from conftest import load_golden
+from fake_engine import OracleEngine
+from nanopow import work as W
+from nanopow.server import HttpWorkServer, WorkServer
+
+LOW = 0xfffff00000000000
+
+
+def post(addr, obj, timeout=30):
+    req = urllib.request.Request(f"http://{addr}", data=json.dumps(obj).encode(),
+                                 headers={"Content-Type": "application/json"}, method="POST")
+    with urllib.request.urlopen(req, timeout=timeout) as r:
+        assert r.status == 200
+        return json.loads(r.read())
+
+
+@pytest.fixture()
+def server():
+    eng = OracleEngine(chunk=1 << 12, delay=0.001)
+    srv = HttpWorkServer(WorkServer(eng), "127.0.0.1", 0).start()
+    yield srv, eng
+    srv.stop()
+
+
+def test_transcript_replay(server):
+    srv, _ = server
+    t = load_golden("workhandler_transcript.json")
+    reqs = t["requests"]
+    assert [r["action"] for r in reqs] == ["invalid", "work_generate", "work_generate", "work_cancel"]
+    # 1. probe: WorkHandler.start reads ['error']
+    r0 = post(srv.address, reqs[0])
+    assert "error" in r0 and r0["error"] == "Unknown command"
+    assert r0["hint"].startswith("Supported commands: work_generate, work_cancel, work_validate")
+    # 2. generate: ['work'] must re-validate at the requested difficulty
+    g = reqs[1]
+    r1 = post(srv.address, g)
+    root, thr = bytes.fromhex(g["hash"]), int(g["difficulty"], 16)
+    assert set(r1) == {"work", "difficulty", "multiplier"}
+    assert len(r1["work"]) == 16 and r1["work"] == r1["work"].lower()
+    v = oracle.work_value_hashlib(root, int(r1["work"], 16))
+    assert v >= thr and int(r1["difficulty"], 16) == v
+    assert float(r1["multiplier"]) == pytest.approx(W.to_multiplier(v, W.DEFAULT_BASE))
+    # 3./4. a generate that never finishes at this threshold, cancelled from a second connection
+    hold = dict(reqs[2], difficulty="ffffffffffffffff")
+    box = {}
+    th = threading.Thread(target=lambda: box.setdefault("r", post(srv.address, hold)))
+    th.start()
+    time.sleep(0.3)
+    assert post(srv.address, {"action": "status"})["generating"] == "1"
+    assert post(srv.address, reqs[3]) == {}
+    th.join(10)
+    assert box["r"] == {"error": "Cancelled"}
+    assert t["replies"][2] == {"error": "Cancelled"}
+
+
+def test_cancel_queued_request(server):
+    srv, _ = server
+    busy = {"action": "work_generate", "hash": "11" * 32, "difficulty": "ffffffffffffffff"}
+    queued = {"action": "work_generate", "hash": "22" * 32, "difficulty": "ffffffffffffffff"}
+    out = {}
+    t1 = threading.Thread(target=lambda: out.setdefault("a", post(srv.address, busy)))
+    t1.start()
+    time.sleep(0.2)
+    t2 = threading.Thread(target=lambda: out.setdefault("b", post(srv.address, queued)))
+    t2.start()
+    time.sleep(0.2)
+    assert post(srv.address, {"action": "status"}) == {"generating": "1", "queue_size": "1"}
+    assert post(srv.address, {"action": "work_cancel", "hash": "22" * 32}) == {}
+    t2.join(5)
+    assert out["b"] == {"error": "Cancelled"}
+    post(srv.address, {"action": "work_cancel", "hash": "11" * 32})
+    t1.join(5)
+    assert out["a"] == {"error": "Cancelled"}
+    assert post(srv.address, {"action": "status"}) == {"generating": "0", "queue_size": "0"}
+
+
+def test_uppercase_and_lowercase_hash_and_multiplier(server):
+    srv, _ = server
+    root = bytes(range(32))
+    for h in [root.hex(), root.hex().upper()]:
+        r = post(srv.address, {"action": "work_generate", "hash": h, "difficulty": "fffff00000000000"})
+        assert oracle.work_value(root, int(r["work"], 16)) >= LOW
+    # multiplier relative to base fffffff800000000: 1/256 -> threshold ffff f800 0000 0000 - ...
+    r = post(srv.address, {"action": "work_generate", "hash": root.hex(), "multiplier": "0.001"})
+    thr = W.from_multiplier(0.001)
+    assert oracle.work_value(root, int(r["work"], 16)) >= thr
+
+
+def test_work_validate(server):
+    srv, _ = server
+    kat = load_golden("known_answers.json")["cases"][0]
+    r = post(srv.address, {"action": "work_validate", "hash": kat["hash"], "work": kat["work"]})
+    assert r["difficulty"] == kat["value"]
+    assert r["valid_all"] == "0" and r["valid_receive"] == "1" and "valid" not in r
+    r = post(srv.address, {"action": "work_validate", "hash": kat["hash"], "work": kat["work"],
+                           "difficulty": "ffffffc000000000"})
+    assert r["valid"] == "1"
+    r = post(srv.address, {"action": "work_validate", "hash": kat["hash"], "work": kat["work"],
+                           "difficulty": "fffffff800000000"})
+    assert r["valid"] == "0"
+    spec = load_golden("known_answers.json")["cases"][1]
+    r = post(srv.address, {"action": "work_validate", "hash": spec["hash"], "work": spec["work"]})
+    assert r["difficulty"] == "1ce5be0f61328fc2" and r["valid_all"] == "0" and r["valid_receive"] == "0"
+
+
+@pytest.mark.parametrize("req,err,hint", [
+    ({"action": "work_generate"}, "Failed to deserialize JSON", "Hash field missing"),
+    ({"action": "work_generate", "hash": ""}, "Bad block hash", "Hash is empty. Expecting a hex string"),
+    ({"action": "work_generate", "hash": "zz" * 32}, "Bad block hash", "Expecting a hex string"),
+    ({"action": "work_generate", "hash": "00" * 31}, "Bad block hash", "Hash is too short (should be 32 bytes)"),
+    ({"action": "work_generate", "hash": "00" * 33}, "Bad block hash", "Hash is too long (should be 32 bytes)"),
+    ({"action": "work_generate", "hash": "00" * 32, "difficulty": "xyz"}, "Bad difficulty",
+     "Threshold not a valid unsigned long (u64). Example: 'ffffffc000000000'"),
+    ({"action": "work_generate", "hash": "00" * 32, "difficulty": "1" * 17}, "Bad difficulty",
+     "Threshold not a valid unsigned long (u64). Example: 'ffffffc000000000'"),
+    ({"action": "work_generate", "hash": "00" * 32, "multiplier": "-1"}, "Bad multiplier",
+     "Expecting a positive number for multiplier"),
+    ({"action": "work_validate", "hash": "00" * 32}, "Failed to deserialize JSON", "Work field missing"),
+    ({"action": "work_validate", "hash": "00" * 32, "work": "1" * 17}, "Bad work",
+     "Work is too long (should be 8 bytes)"),
+    ({"action": "benchmark"}, "Failed to deserialize JSON", "count field missing"),
+    ({"action": "benchmark", "count": 0}, "Bad count", "Expecting a positive number for count"),
+    ({"action": "nope"}, "Unknown command", W.SUPPORTED),
+])
+def test_error_replies(server, req, err, hint):
+    srv, _ = server
+    r = post(srv.address, req)
+    assert r == {"error": err, "hint": hint}
+
+
+def test_non_json_and_get(server):
+    srv, _ = server
+    req = urllib.request.Request(f"http://{srv.address}", data=b"{not json", method="POST")
+    with urllib.request.urlopen(req, timeout=5) as r:
+        assert json.loads(r.read()) == {"error": "Failed to deserialize JSON"}
+    with pytest.raises(urllib.error.HTTPError) as ei:
+        urllib.request.urlopen(f"http://{srv.address}", timeout=5)
+    assert json.loads(ei.value.read()) == {"error": "Can only POST requests"}
+
+
+def test_benchmark(server):
+    srv, _ = server
+    r = post(srv.address, {"action": "benchmark", "count": 3, "difficulty": "ffff000000000000"})
+    assert r["count"] == "3" and r["hint"] == "Times in milliseconds"
+    assert int(r["duration"]) >= 0 and int(r["average"]) >= 0
+
+
+def test_duplicate_requests_share_one_search(server):
+    srv, eng = server
+    root = "ab" * 32
+    req = {"action": "work_generate", "hash": root, "difficulty": "ffffff0000000000"}
+    # occupy the worker so both duplicates queue behind it
+    hold = {"action": "work_generate", "hash": "cd" * 32, "difficulty": "ffffffffffffffff"}
+    th0 = threading.Thread(target=lambda: post(srv.address, hold))
+    th0.start()
+    time.sleep(0.2)
+    res = []
+    ths = [threading.Thread(target=lambda: res.append(post(srv.address, req))) for _ in range(2)]
+    for t in ths:
+        t.start()
+    time.sleep(0.3)
+    assert post(srv.address, {"action": "status"})["queue_size"] == "1"
+    post(srv.address, {"action": "work_cancel", "hash": "cd" * 32})
+    for t in ths:
+        t.join(30)
+    th0.join(5)
+    assert len(res) == 2 and res[0] == res[1] and "work" in res[0]
+    assert sum(1 for c in eng.calls if c[0] == bytes.fromhex(root)) == 1
+
+
+def test_shuffle_picks_all_requests():
+    eng = OracleEngine()
+    ws = WorkServer(eng, shuffle=True).start()
+    try:
+        out = []
+        ths = [threading.Thread(target=lambda i=i: out.append(
+            ws.handle({"action": "work_generate", "hash": f"{i:064x}", "difficulty": "ffff000000000000"})))
+            for i in range(6)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(30)
+        assert len(out) == 6 and all("work" in r for r in out)
+    finally:
+        ws.stop()

@@ -1,0 +1,54 @@
+"""Host logic: threshold / multiplier math and CLI parsing (CPU)."""
+import pytest
+
+from nanopow import work as W
+from nanopow.__main__ import parse_args
+
+
+def test_multiplier_roundtrip_dpow_formulas():
+    # dpow_server.py:250-255 / 275-280: multiplier = (2^64-base)/(2^64-d), d = 2^64-(2^64-base)/m
+    base = W.DEFAULT_BASE
+    assert W.to_multiplier(base, base) == 1.0
+    assert W.from_multiplier(1.0, base) == base
+    assert W.to_multiplier(W.RECEIVE_THRESHOLD, base) == pytest.approx(1 / 64)
+    assert W.from_multiplier(1 / 64, base) == W.RECEIVE_THRESHOLD
+    assert W.from_multiplier(8.0, base) == 0xffffffff00000000
+    for m in [0.5, 1.5, 2.0, 7.3]:
+        assert W.to_multiplier(W.from_multiplier(m, base), base) == pytest.approx(m, rel=1e-9)
+
+
+def test_threshold_parsing():
+    assert W.parse_threshold("fffffff800000000") == W.SEND_THRESHOLD
+    assert W.parse_threshold("FFFFFE0000000000") == W.RECEIVE_THRESHOLD
+    assert W.parse_threshold("0") == 0
+    for bad in ["", "g", "-1", "1" * 17, 5]:
+        with pytest.raises(W.RequestError):
+            W.parse_threshold(bad)
+
+
+def test_requested_threshold_precedence():
+    assert W.requested_threshold({}, 123) == 123
+    assert W.requested_threshold({"multiplier": 1}, W.DEFAULT_BASE) == W.DEFAULT_BASE
+    assert W.requested_threshold({"difficulty": "ff", "multiplier": 2}, W.DEFAULT_BASE) == 0xff
+
+
+def test_work_and_hash_parsing():
+    assert W.parse_hash({"hash": "AB" * 32}) == b"\xab" * 32
+    assert W.parse_work({"work": "62f05417dd3fb691"}) == 0x62f05417dd3fb691
+    assert W.parse_work({"work": "1"}) == 1
+    assert W.fmt_u64(1) == "0000000000000001"
+
+
+def test_gpu_spec_and_cli():
+    assert W.parse_gpu_spec("0:0") == (0, 0, 1048576)
+    assert W.parse_gpu_spec("0:3:4194304") == (0, 3, 4194304)
+    with pytest.raises(ValueError):
+        W.parse_gpu_spec("0")
+    a = parse_args(["--gpu", "0:0", "-l", "127.0.0.1:7000", "--shuffle", "--gpu-local-work-size", "64"])
+    assert a.gpu == ["0:0"] and a.listen == "127.0.0.1:7000" and a.shuffle and a.local_work_size == 64
+    assert parse_args([]).listen == "127.0.0.1:7000"
+
+
+def test_cpu_threads_rejected():
+    from nanopow.__main__ import main
+    assert main(["--cpu-threads", "4"]) == 2
