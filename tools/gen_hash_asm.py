@@ -260,7 +260,14 @@ def lower(dag: Dag, out: Node):
 
 
 # issue cost (SIMD cycles per wave64 instruction, profiles/r01_valu_ubench.json) and latency model
-COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b32": 4.3, "v_lshl_add_u64": 4.4}
+COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b32": 4.3, "v_lshl_add_u64": 4.4,
+        "v_lshrrev_b32": 2.5, "v_mov_b32": 2.4}
+ROTL1_VIA_ADD = True  # rotr63 = (x << 1) + (x >> 63): v_lshrrev_b32 + v_lshl_add_u64 with a zero partner
+# Measured on MI355X (tools/valu_patterns.py): in a stream that mixes in 64-bit / 3-operand VALU
+# ops, VOP2-encoded v_xor_b32 issues at ~4.1 SIMD cycles but its VOP3 (_e64) encoding at ~2.6.
+VOP3_SIMPLE = True
+# rotr32 as two in-place xors + two v_mov_b32 into the fresh pair (movs issue nearly free)
+SWAP_MOV = False
 LAT = 8.0
 
 
@@ -274,6 +281,8 @@ def op_cost(op: Op) -> float:
     if op.kind == "add":
         return COST["v_lshl_add_u64"]
     x = 2 * max(xc(op.srcs[0]), xc(op.srcs[1]))
+    if op.kind == "xrot" and op.n == 63 and ROTL1_VIA_ADD:
+        return x + COST["v_lshrrev_b32"] + COST["v_lshl_add_u64"]
     if op.kind == "xrot":
         return x + 2 * COST["v_alignbit_b32"]
     return x
@@ -358,6 +367,15 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
                 remaining[s.id] = remaining.get(s.id, 0) + 1
     al = Alloc(base, limit)
     loc: Dict[int, int] = {}  # node id -> even base register of its pair
+    # {t, 0} pairs for rotr63 = (x << 1) + (x >> 63): the odd register of each holds zero
+    zpairs = []
+    lines_pre: List[str] = []
+    if ROTL1_VIA_ADD:
+        for _ in range(2):
+            r = al.take2()
+            zpairs.append(r)
+            lines_pre.append(f"v_mov_b32 v{r + 1}, 0")
+    zturn = [0]
     NONCE = "%[nonce]"
     lines: List[str] = []
     counts: Dict[str, int] = {}
@@ -429,6 +447,24 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             loc[op.dst.id] = r
             lines.append(f"v_lshl_add_u64 v[{r}:{r + 1}], {ta}, 0, {tb}")
             cnt("v_lshl_add_u64")
+        elif op.kind == "xrot32" and SWAP_MOV:
+            s0h, s1h = xor_operands(a, b, 1)
+            s0l, s1l = xor_operands(a, b, 0)
+            consume(op)
+            tl = al.take1()
+            th = al.take1(avoid=(tl,))
+            lines.append(f"v_xor_b32 v{tl}, {s0l}, {s1l}")
+            lines.append(f"v_xor_b32 v{th}, {s0h}, {s1h}")
+            r = al.take2(avoid=(tl, th))
+            loc[op.dst.id] = r
+            lines.append(f"v_mov_b32 v{r}, v{th}")
+            lines.append(f"v_mov_b32 v{r + 1}, v{tl}")
+            al.release(tl)
+            al.release(th)
+            cnt("v_xor_b32")
+            cnt("v_xor_b32")
+            cnt("v_mov_b32")
+            cnt("v_mov_b32")
         elif op.kind == "xrot32":
             # dst.lo = a.hi ^ b.hi ; dst.hi = a.lo ^ b.lo  (rotation by 32 is the swap).
             # dst.lo is written before the lo halves are read: keep it off them.
@@ -442,6 +478,22 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             lines.append(f"v_xor_b32 v{r + 1}, {s0l}, {s1l}")
             cnt("v_xor_b32")
             cnt("v_xor_b32")
+        elif op.kind == "xrot" and op.n == 63 and ROTL1_VIA_ADD:
+            s0l, s1l = xor_operands(a, b, 0)
+            s0h, s1h = xor_operands(a, b, 1)
+            consume(op)
+            r = al.take2()  # x = a ^ b: lo written first (hi sources are odd registers, never r)
+            lines.append(f"v_xor_b32 v{r}, {s0l}, {s1l}")
+            lines.append(f"v_xor_b32 v{r + 1}, {s0h}, {s1h}")
+            z = zpairs[zturn[0] % len(zpairs)]
+            zturn[0] += 1
+            lines.append(f"v_lshrrev_b32 v{z}, 31, v{r + 1}")
+            lines.append(f"v_lshl_add_u64 v[{r}:{r + 1}], v[{r}:{r + 1}], 1, v[{z}:{z + 1}]")
+            loc[op.dst.id] = r
+            cnt("v_xor_b32")
+            cnt("v_xor_b32")
+            cnt("v_lshrrev_b32")
+            cnt("v_lshl_add_u64")
         elif op.kind == "xrot":
             s0l, s1l = xor_operands(a, b, 0)
             s0h, s1h = xor_operands(a, b, 1)
@@ -483,7 +535,18 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             cnt("v_xor_b32")
         else:
             raise ValueError(op.kind)
-    return lines, uni_index, al.max_used, counts
+    for ln in lines_pre:
+        cnt(ln.split(" ", 1)[0])
+    out_lines = lines_pre + lines
+    if VOP3_SIMPLE:
+        conv = []
+        for ln in out_lines:
+            opc, rest = ln.split(" ", 1)
+            if opc in ("v_xor_b32", "v_lshrrev_b32") and "0x" not in rest:
+                opc += "_e64"
+            conv.append(f"{opc} {rest}")
+        out_lines = conv
+    return out_lines, uni_index, al.max_used, counts
 
 
 # ---------------------------------------------------------------------------------------
@@ -526,14 +589,19 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
 
     for ln in lines:
         opc, rest = ln.split(" ", 1)
+        opc = opc[:-4] if opc.endswith("_e64") else opc
         ops = [t.strip() for t in rest.split(",")]
         if opc == "v_xor_b32":
             wr32(ops[0], rd32(ops[1]) ^ rd32(ops[2]))
         elif opc == "v_alignbit_b32":
             hi, lo, sh = rd32(ops[1]), rd32(ops[2]), int(ops[3])
             wr32(ops[0], (((hi << 32) | lo) >> sh) & M32)
+        elif opc == "v_lshrrev_b32":
+            wr32(ops[0], rd32(ops[2]) >> int(ops[1]))
+        elif opc == "v_mov_b32":
+            wr32(ops[0], rd32(ops[1]))
         elif opc == "v_lshl_add_u64":
-            x = rd64(ops[1]) << int(ops[2])
+            x = (rd64(ops[1]) << int(ops[2])) & M64
             y = rd64(ops[3])
             s = (x + y) & M64
             lo = int(ops[0][2:-1].split(":")[0])
@@ -648,7 +716,16 @@ def main() -> int:
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                                   "nano-dpow_amd", "csrc", "npow_hash_asm.inc"))
     ap.add_argument("--check", type=int, default=64, help="random (root, nonce) pairs to check vs hashlib")
+    ap.add_argument("--rotl1", choices=["add", "alignbit"], default="add",
+                    help="rotr63 as v_lshrrev_b32 + v_lshl_add_u64 (add) or two v_alignbit_b32")
+    ap.add_argument("--enc", choices=["vop3", "vop2"], default="vop3",
+                    help="encoding of the simple 32-bit ops (xor, lshrrev)")
+    ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
     args = ap.parse_args()
+    global ROTL1_VIA_ADD, VOP3_SIMPLE, SWAP_MOV
+    SWAP_MOV = args.swapmov
+    ROTL1_VIA_ADD = args.rotl1 == "add"
+    VOP3_SIMPLE = args.enc == "vop3"
 
     dag, out = build_hash_dag()
     ops, frontier, _ = lower(dag, out)
@@ -657,6 +734,7 @@ def main() -> int:
     est = 0.0
     for ln in lines:
         opc = ln.split(" ", 1)[0]
+        opc = opc[:-4] if opc.endswith("_e64") else opc
         if opc == "v_xor_b32":
             src0 = ln.split(",")[1].strip()
             est += COST["v_xor_b32_k"] if src0.startswith("0x") else (
@@ -675,7 +753,7 @@ def main() -> int:
             print(f"MISMATCH root={root.hex()} nonce={nonce:016x} got={got:016x} want={want:016x}")
             return 1
     host_prog = c_expr_program(frontier)
-    write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, args.sched, est)
+    write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --enc {args.enc}" + (" --swapmov" if args.swapmov else ""), est)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
           f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")
     return 0
