@@ -94,6 +94,87 @@ def cpu_baseline(seconds: float = 12.0):
             "hashlib_1core_gnps": round(hl / 1e9, 6)}
 
 
+def run_timed(search, stats, reset_stats, steps: int, warmup: int, rank: int, world: int, dist=None):
+    """Warm up, then time exactly `steps` searches bracketed by barriers; reduce over ranks.
+
+    search(i) -> (seconds, nonces_hashed); stats() -> (kernel_ms, kernel_nonces, launches).
+    Returns the rank-0 view: (total_nonces, max_wall_s, all_ttw_s, kernel_ms, kernel_nonces, launches)
+    with kernel_* summed over ranks."""
+    base_idx = 1_000_000 * (rank + 1)
+    for w in range(warmup):
+        search(base_idx + 900_000 + w)
+    reset_stats()
+    if dist is not None:
+        dist.barrier()
+    # npow_search returns only after its streams drained, so the GPU is idle at both barriers
+    t0 = time.perf_counter()
+    ttw, nonces = [], 0
+    for s in range(steps):
+        dt, n = search(base_idx + s)
+        ttw.append(dt)
+        nonces += n
+    if dist is not None:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    kern_ms, kern_nonces, launches = stats()
+    if dist is None:
+        return nonces, wall, ttw, kern_ms, kern_nonces, launches
+    import torch
+    v = torch.tensor([float(nonces), float(kern_ms), float(kern_nonces), float(launches)], dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    w_t = torch.tensor([wall], dtype=torch.float64)
+    dist.all_reduce(w_t, op=dist.ReduceOp.MAX)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, ttw)
+    all_ttw = [x for g in gathered for x in g]
+    return int(v[0]), float(w_t[0]), all_ttw, float(v[1]), int(v[2]), int(v[3])
+
+
+def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, kern_nonces, launches):
+    gnps = tot_nonces / max_wall / 1e9
+    per_rank_kernel_s = kern_ms * 1e-3 / world
+    achieved = (kern_nonces / world) * OPS_PER_NONCE / per_rank_kernel_s / 1e12 if kern_ms > 0 else 0.0
+    return {
+        "metric": METRIC,
+        "value": round(gnps, 4),
+        "unit": "Gnonce/s",
+        "n_gpus": world,
+        "steps": steps,
+        "warmup": warmup,
+        "ms_per_step": round(max_wall / steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u64",
+        "data": "synthetic (random-looking 32-byte roots R_i = blake2b(b'nanopow-bench'+LE64(i)))",
+        "config": {
+            "workload": "BASELINE configs[1]: single block hash per search at send difficulty "
+                        "fffffff800000000, first-win search, p50/p99 time-to-work",
+            "threshold": "fffffff800000000",
+            "searches_per_gpu": steps,
+            "parallelism": f"dp{world} (disjoint roots per GPU, no collective)",
+        },
+        "p50_ttw_ms": round(pct(all_ttw, 50) * 1e3, 3),
+        "p99_ttw_ms": round(pct(all_ttw, 99) * 1e3, 3),
+        "mean_ttw_ms": round(statistics.mean(all_ttw) * 1e3, 3),
+        "gnps_per_gpu": round(gnps / world, 4),
+        "roofline": {
+            "bound": "valu",
+            "kernel": "npow_task_kernel<Mode::kSearch>",
+            "achieved": round(achieved, 3),
+            "peak": round(PEAK_TOPS, 3),
+            "unit": "Tops/s (int32 VALU)",
+            "frac": round(achieved / PEAK_TOPS, 4),
+            "traffic": None,
+            "ops_per_nonce": OPS_PER_NONCE,
+            "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
+            "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
+            "launches": launches,
+        },
+        "cpu_baseline": None,
+    }
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -116,93 +197,21 @@ def main() -> int:
         eng.set_tuning(args.iters, 0, 0)
     dev = 0
 
-    def barrier_sync():
-        if dist is not None:
-            dist.barrier()
-        # npow_search returns only after its streams drained: the device is idle here.
-
-    def one(i):
+    def search(i):
         t = time.perf_counter()
         r = eng.search(bench_root(i), SEND, start=bench_start(i), device_mask=1 << dev)
         dt = time.perf_counter() - t
         if r.status != _lib.NPOW_OK:
             raise RuntimeError(f"search {i} returned status {r.status}")
-        return dt, r
+        return dt, r.nonces_done
 
-    base_idx = 1_000_000 * (rank + 1)
-    for w in range(args.warmup):
-        one(base_idx + 900_000 + w)
-    eng.reset_stats(dev)
-    barrier_sync()
-    t0 = time.perf_counter()
-    ttw, nonces = [], 0
-    for s in range(args.steps):
-        dt, r = one(base_idx + s)
-        ttw.append(dt)
-        nonces += r.nonces_done
-    barrier_sync()
-    wall = time.perf_counter() - t0
-    st = eng.stats(dev)
+    def stats():
+        st = eng.stats(dev)
+        return st.kernel_ms, st.nonces, st.launches
 
-    # validate every winner of rank 0's first searches against the product's CPU check path
-    all_ttw = ttw
-    tot_nonces, max_wall, kern_ms, kern_nonces, launches = nonces, wall, st.kernel_ms, st.nonces, st.launches
-    if dist is not None:
-        import torch
-        v = torch.tensor([float(nonces), float(st.kernel_ms), float(st.nonces), float(st.launches)],
-                         dtype=torch.float64)
-        dist.all_reduce(v, op=dist.ReduceOp.SUM)
-        w_t = torch.tensor([wall], dtype=torch.float64)
-        dist.all_reduce(w_t, op=dist.ReduceOp.MAX)
-        gathered = [None] * WORLD
-        dist.all_gather_object(gathered, ttw)
-        all_ttw = [x for g in gathered for x in g]
-        tot_nonces, kern_ms, kern_nonces, launches = int(v[0]), float(v[1]), int(v[2]), int(v[3])
-        max_wall = float(w_t[0])
-
+    res = run_timed(search, stats, lambda: eng.reset_stats(dev), args.steps, args.warmup, rank, WORLD, dist)
     if rank == 0:
-        gnps = tot_nonces / max_wall / 1e9
-        per_rank_kernel_s = kern_ms * 1e-3 / WORLD
-        achieved = (kern_nonces / WORLD) * OPS_PER_NONCE / per_rank_kernel_s / 1e12 if kern_ms > 0 else 0.0
-        line = {
-            "metric": METRIC,
-            "value": round(gnps, 4),
-            "unit": "Gnonce/s",
-            "n_gpus": WORLD,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(max_wall / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "u64",
-            "data": "synthetic (random-looking 32-byte roots R_i = blake2b(b'nanopow-bench'+LE64(i)))",
-            "config": {
-                "workload": "BASELINE configs[1]: single block hash per search at send difficulty "
-                            "fffffff800000000, first-win search, p50/p99 time-to-work",
-                "threshold": "fffffff800000000",
-                "searches_per_gpu": args.steps,
-                "parallelism": f"dp{WORLD} (disjoint roots per GPU, no collective)",
-            },
-            "p50_ttw_ms": round(pct(all_ttw, 50) * 1e3, 3),
-            "p99_ttw_ms": round(pct(all_ttw, 99) * 1e3, 3),
-            "mean_ttw_ms": round(statistics.mean(all_ttw) * 1e3, 3),
-            "gnps_per_gpu": round(gnps / WORLD, 4),
-            "roofline": {
-                "bound": "valu",
-                "kernel": "npow_task_kernel<Mode::kSearch>",
-                "achieved": round(achieved, 3),
-                "peak": round(PEAK_TOPS, 3),
-                "unit": "Tops/s (int32 VALU)",
-                "frac": round(achieved / PEAK_TOPS, 4),
-                "traffic": None,
-                "ops_per_nonce": OPS_PER_NONCE,
-                "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
-                "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
-                "launches": launches,
-            },
-            "cpu_baseline": None,
-        }
+        line = result_line(WORLD, args.steps, args.warmup, *res)
         if WORLD == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)

@@ -1,0 +1,79 @@
+"""World-size-2 gloo run of bench.py's timed region + reductions (CPU; the GPU search is
+replaced by an oracle search).  Checks the contract: value = all ranks' nonces / MAX wall,
+ttw gathered from every rank, kernel counters summed; and the per-GPU nonce strides of the
+in-process multi-device search are disjoint."""
+import os
+import socket
+import sys
+
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+sys.path.insert(0, ROOT)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bench
+    import oracle
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def search(i):
+        import time
+        t = time.perf_counter()
+        scanned, nonce = oracle.search(bench.bench_root(i), 0xffff000000000000, bench.bench_start(i), 1 << 22)
+        assert nonce is not None
+        return time.perf_counter() - t + (0.01 if rank == 1 else 0.0), scanned
+
+    res = bench.run_timed(search, lambda: (10.0 * (rank + 1), 1000 * (rank + 1), 2), lambda: None,
+                          steps=5, warmup=1, rank=rank, world=world, dist=dist)
+    line = bench.result_line(world, 5, 1, *res)
+    q.put((rank, res, line))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_gloo_bench_reduction():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in range(2):
+        r, res, line = q.get(timeout=120)
+        out[r] = (res, line)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    (n0, w0, ttw0, km0, kn0, l0), line0 = out[0]
+    (n1, w1, ttw1, km1, kn1, l1), _ = out[1]
+    assert n0 == n1 and w0 == w1          # every rank holds the reduced values
+    assert len(ttw0) == 10                # gathered from both ranks
+    assert km0 == 30.0 and kn0 == 3000 and l0 == 4
+    assert line0["n_gpus"] == 2 and line0["scaling"] == "weak"
+    assert line0["value"] == round(n0 / w0 / 1e9, 4)
+    assert line0["roofline"]["unit"].startswith("Tops/s")
+
+
+def test_device_strides_disjoint():
+    # npow_search: device k of G starts at start + k * (2^64 / G)  (npow_engine.cpp)
+    for G in [1, 2, 3, 4, 8]:
+        spacing = ((1 << 64) - 1) // G + 1 if G > 1 else 0
+        starts = [(k * spacing) % (1 << 64) for k in range(G)]
+        assert len(set(starts)) == G
+        if G > 1:
+            assert all(b - a >= (1 << 64) // G for a, b in zip(starts, starts[1:]))
