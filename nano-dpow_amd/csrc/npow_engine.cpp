@@ -139,7 +139,7 @@ int read_state(Device& d, DevState* hs) {
   HIPTRY(hipMemcpyAsync(hs, d.st, sizeof(DevState), hipMemcpyDeviceToHost, d.stream));
   HIPTRY(hipStreamSynchronize(d.stream));
   std::lock_guard<std::mutex> g(d.stats_mu);
-  d.nonces += hs->done;
+  d.nonces += hs->done();
   return NPOW_OK;
 }
 
@@ -235,7 +235,7 @@ int device_search(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_
         DevState hs;
         rc = read_state(d, &hs);
         if (rc) return rc;
-        total_done += hs.done;
+        total_done += hs.done();
         if (++invalid_streak >= 3) {
           d.dead = true;
           sh.done += total_done;
@@ -277,7 +277,7 @@ int device_search(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_
   DevState hs;
   rc = read_state(d, &hs);
   if (rc) return rc;
-  total_done += hs.done;
+  total_done += hs.done();
   sh.done += total_done;
   return NPOW_OK;
 }

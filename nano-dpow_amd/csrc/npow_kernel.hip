@@ -136,10 +136,16 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
     //  wait on it.
     uint64_t stop_word = 0;
     uint32_t host_abort = 0;
+#ifndef NPOW_POLL_MODE
+#define NPOW_POLL_MODE 2
+#endif
     if constexpr (MODE != Mode::kValues) {
-      stop_word = __hip_atomic_load(&st->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t* poll = ((iter + wave_id) & a.poll_mask) == 0 ? &mb->abort : &st->zero;
-      host_abort = __hip_atomic_load(poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (NPOW_POLL_MODE >= 1)
+        stop_word = __hip_atomic_load(&st->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (NPOW_POLL_MODE >= 2) {
+        const uint32_t* poll = ((iter + wave_id) & a.poll_mask) == 0 ? &mb->abort : &st->zero;
+        host_abort = __hip_atomic_load(poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
     }
 
     const uint64_t i = ib + lane;
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
       if (__builtin_amdgcn_readfirstlane((uint32_t)stop_word | (uint32_t)(stop_word >> 32))) break;
     }
   }
-  if (lane == 0 && done) atomicAdd(&st->done, (unsigned long long)done);
+  if (lane == 0 && done) atomicAdd(&st->done_shard[(blockIdx.x % kDoneShards) * 8], (unsigned long long)done);
 }
 
 __global__ __launch_bounds__(kBlock) void npow_pairs_kernel(const uint64_t* __restrict__ roots_words,
