@@ -75,7 +75,7 @@ std::mutex g_mu;
 bool g_init = false;
 std::vector<std::unique_ptr<Device>> g_devs;
 std::atomic<uint32_t> g_iters{256};     // wave iterations per launch (2^27 nonces at 2048 x 256 lanes)
-std::atomic<uint32_t> g_poll{64};       // a wave reads the host abort word every g_poll iterations (power of two)
+std::atomic<uint32_t> g_poll{1024};     // a wave reads the host abort word every g_poll iterations (8 waves per iteration grid-wide)
 std::atomic<uint32_t> g_blocks_per_cu{8};
 
 int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }

@@ -125,15 +125,16 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
   uint32_t iter = 0;
 
   for (uint64_t ib = wave0; ib < a.count; ib += stride, ++iter) {
-    // Early-exit polls, issued first so their latency hides under the hash:
+    // Early-exit polls:
     //  * every iteration, one agent-scope (L2) load of the device stop word
-    //    {found, abort} -- set by a winning wave or relayed from the host;
-    //  * the host abort word lives in pinned host memory (a PCIe read), so only
-    //    one wave in poll_mask+1 reads it per iteration (staggered by wave id)
-    //    and relays a raised abort into the device stop word.
-    //  On iterations where this wave does not poll the host, the same load
-    //  reads an always-zero device word instead, so no branch forces an early
-    //  wait on it.
+    //    {found, abort} -- set by a winning wave or relayed from the host; it is
+    //    issued first and consumed after the hash, so its latency is hidden;
+    //  * the host abort word lives in pinned host memory (a PCIe read whose
+    //    latency and throughput vary by host: on some boxes thousands of
+    //    concurrent reads queue up for tens of microseconds), so only one wave in
+    //    poll_mask+1 reads it per iteration (staggered by wave id: with the
+    //    default 1024 that is 8 waves per iteration grid-wide) and relays a raised
+    //    abort into the device stop word.
     uint64_t stop_word = 0;
     uint32_t host_abort = 0;
 #ifndef NPOW_POLL_MODE
@@ -142,10 +143,8 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
     if constexpr (MODE != Mode::kValues) {
       if (NPOW_POLL_MODE >= 1)
         stop_word = __hip_atomic_load(&st->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (NPOW_POLL_MODE >= 2) {
-        const uint32_t* poll = ((iter + wave_id) & a.poll_mask) == 0 ? &mb->abort : &st->zero;
-        host_abort = __hip_atomic_load(poll, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
+      if (NPOW_POLL_MODE >= 2 && ((iter + wave_id) & a.poll_mask) == 0)
+        host_abort = __hip_atomic_load(&mb->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 
     const uint64_t i = ib + lane;
