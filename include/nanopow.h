@@ -37,6 +37,7 @@ extern "C" {
 #define NPOW_OK 0
 #define NPOW_CANCELLED 1
 #define NPOW_EXHAUSTED 2
+#define NPOW_PENDING 3             /* npow_wait: timeout elapsed, the ticket is still valid */
 #define NPOW_ERR_NOT_INITIALISED (-1)
 #define NPOW_ERR_NO_DEVICE (-2)
 #define NPOW_ERR_BAD_ARGUMENT (-3)
@@ -74,12 +75,14 @@ uint64_t npow_work_value(const uint8_t root[32], uint64_t nonce);
 /* First-win search: scan the nonce space from `start` on every device in
  * `device_mask` (device k of G starts at start + k*2^64/G, disjoint strides) until one
  * value >= threshold is found (NPOW_OK), `*cancel` becomes non-zero
- * (NPOW_CANCELLED), or every device's stride of `max_nonces_per_device`
- * (0 = unbounded) is exhausted (NPOW_EXHAUSTED).
+ * (NPOW_CANCELLED), or every device's range [start_k, start_k + max_nonces_per_device)
+ * (0 = unbounded) has been hashed without a hit (NPOW_EXHAUSTED).
  * Replaces the kernel `nano_work` (nano-work-server.exe @1661643) and the work
  * server's GPU loop behind `work_generate` (@1673856 reply fields work /
  * difficulty / multiplier, "Cancelled" @1673856).  Every GPU winner is
  * re-validated on the CPU before it is returned.
+ * The search is a job of the engine's work pool (= npow_submit + npow_wait): it runs
+ * in the same kernel launches as every other job in flight on those devices.
  * `cancel` may be NULL.  `nonces_done` (may be NULL) receives the number of
  * nonces hashed by all devices, including the rest of a chunk after the win. */
 int npow_search(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
@@ -89,13 +92,44 @@ int npow_search(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
 /* Batched first-win search over n roots (the DPoW burst: many work_generate
  * requests in flight at once, client/work_handler.py:83-125 per client).
  * Each root i gets its own threshold and its own cancel word cancel[i]
- * (cancel itself or any entry may be NULL).  Roots are dealt round-robin over
- * the devices in device_mask; status_out[i] is NPOW_OK / NPOW_CANCELLED /
- * NPOW_EXHAUSTED per root.  Returns NPOW_OK or a negative error. */
+ * (cancel itself or any entry may be NULL) and is searched by every device in
+ * device_mask; up to the pool's max_active roots share each kernel launch.
+ * status_out[i] is NPOW_OK / NPOW_CANCELLED / NPOW_EXHAUSTED (or an error) per
+ * root; *nonces_done = nonces hashed for all roots.  Returns NPOW_OK or the
+ * first negative error. */
 int npow_search_batch(const uint8_t* roots, const uint64_t* thresholds, uint32_t n,
                       uint64_t device_mask, uint64_t max_nonces_per_root,
                       const volatile uint32_t* const* cancel, uint64_t* nonces_out,
                       uint64_t* values_out, int32_t* status_out, uint64_t* nonces_done);
+
+/* ---- Work pool: asynchronous first-win searches ----------------------------------
+ * Every search is a job of the engine's pool.  Jobs queue FIFO; up to max_active
+ * (default and maximum 64) are live at once, and each device searches all of its
+ * live jobs in ONE kernel launch (a job won or cancelled mid-launch hands its waves
+ * to the others).  Replaces the work server's request queue (nano-work-server.exe
+ * @1679680 `status` generating / queue_size) with concurrent service.
+ *
+ * npow_submit: queue a search (arguments as npow_search) and return at once with a
+ * ticket.  `cancel` (may be NULL) must stay valid until npow_wait returns a final
+ * status for the ticket. */
+int npow_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
+                uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket);
+
+/* Wait up to timeout_us (< 0: forever) for a ticket.  Returns NPOW_PENDING on timeout
+ * (the ticket stays valid), otherwise the search's final status exactly as npow_search
+ * returns it; the ticket is released then.  Outputs as npow_search. */
+int npow_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce_out, uint64_t* value_out,
+              uint64_t* nonces_done);
+
+/* Cancel a ticket (same effect as raising its cancel word). */
+int npow_cancel(uint64_t ticket);
+
+/* Jobs searched at once (1..64).  Fewer gives the oldest requests every GPU sooner
+ * (lower time-to-work under load); more keeps waves busy when jobs end mid-launch. */
+int npow_pool_config(uint32_t max_active);
+
+/* Jobs queued (not yet live) and live. */
+int npow_pool_status(uint32_t* queued, uint32_t* active);
 
 /* Exhaustive sweep: every nonce in [start, start+count) (mod 2^64) whose value
  * >= threshold, written to out[0..min(n,cap)) in ascending (nonce - start)

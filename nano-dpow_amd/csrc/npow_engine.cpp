@@ -17,9 +17,9 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -28,73 +28,24 @@
 #include <thread>
 #include <vector>
 
-#include "../../include/nanopow.h"
-#include "npow_blake2b.h"
-#include "npow_internal.h"
+#include "npow_host.h"
 
 namespace npow {
-namespace {
 
+namespace {
 thread_local std::string t_err;
+}  // namespace
 
 int fail(int code, const std::string& msg) {
   t_err = msg;
   return code;
 }
+const std::string& last_error() { return t_err; }
 
-#define HIPTRY(expr)                                                                        \
-  do {                                                                                      \
-    hipError_t e_ = (expr);                                                                 \
-    if (e_ != hipSuccess)                                                                   \
-      return fail(NPOW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));          \
-  } while (0)
-
-constexpr int kEventRing = 4;
-constexpr uint64_t kHitCap = 1u << 20;        // per-device sweep hit buffer (8 MiB)
-constexpr uint64_t kValuesChunk = 1u << 24;   // values mode: nonces per launch (128 MiB out)
-
-struct Device {
-  int id = 0;
-  int cus = 0;
-  hipStream_t stream = nullptr;
-  DevState* st = nullptr;        // device memory
-  HostMailbox* mb = nullptr;     // pinned host (coherent), host view
-  HostMailbox* mb_dev = nullptr; // device view of the same bytes
-  uint64_t* d_out = nullptr;     // sweep hits / values (kValuesChunk entries)
-  hipEvent_t ev_start[kEventRing] = {};
-  hipEvent_t ev_stop[kEventRing] = {};
-  std::mutex mu;                 // one task per device at a time
-  // statistics
-  std::mutex stats_mu;
-  uint64_t launches = 0, nonces = 0, invalid = 0;
-  double kernel_ms = 0.0;
-  bool dead = false;
-};
-
-std::mutex g_mu;
-bool g_init = false;
 std::vector<std::unique_ptr<Device>> g_devs;
 std::atomic<uint32_t> g_iters{256};     // wave iterations per launch (2^27 nonces at 2048 x 256 lanes)
-std::atomic<uint32_t> g_poll{1024};     // a wave reads the host abort word every g_poll iterations (8 waves per iteration grid-wide)
+std::atomic<uint32_t> g_poll{1024};     // a wave reads the host word every g_poll iterations (8 waves per iteration grid-wide)
 std::atomic<uint32_t> g_blocks_per_cu{8};
-
-int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }
-
-uint32_t poll_mask() {
-  uint32_t p = g_poll.load();
-  uint32_t m = 1;
-  while (m < p) m <<= 1;
-  return m - 1;
-}
-
-void store_release(volatile uint32_t* p, uint32_t v) { __atomic_store_n((uint32_t*)p, v, __ATOMIC_RELEASE); }
-uint32_t load_acquire(const volatile uint32_t* p) { return __atomic_load_n((const uint32_t*)p, __ATOMIC_ACQUIRE); }
-
-void cpu_relax() {
-#if defined(__x86_64__)
-  __builtin_ia32_pause();
-#endif
-}
 
 std::vector<Device*> select_devices(uint64_t mask) {
   std::vector<Device*> out;
@@ -102,6 +53,22 @@ std::vector<Device*> select_devices(uint64_t mask) {
     if ((mask == 0 || (mask >> d->id) & 1ull) && !d->dead) out.push_back(d.get());
   return out;
 }
+
+void account_launch(Device& d, int ring) {
+  float ms = 0.f;
+  if (hipEventElapsedTime(&ms, d.ev_start[ring], d.ev_stop[ring]) != hipSuccess) ms = 0.f;
+  std::lock_guard<std::mutex> g(d.stats_mu);
+  d.launches++;
+  d.kernel_ms += ms;
+}
+
+namespace {
+
+std::mutex g_mu;
+bool g_init = false;
+
+constexpr uint64_t kHitCap = 1u << 20;        // per-device sweep hit buffer (8 MiB)
+constexpr uint64_t kValuesChunk = 1u << 24;   // values mode: nonces per launch (128 MiB out)
 
 // One in-flight launch.
 struct Inflight {
@@ -115,14 +82,6 @@ int launch_chunk(Device& d, Mode mode, const LaunchArgs& a, int ring, uint64_t* 
   HIPTRY(launch_task(mode, grid_of(d), d.stream, a, d.st, d.mb_dev, out));
   HIPTRY(hipEventRecord(d.ev_stop[ring], d.stream));
   return NPOW_OK;
-}
-
-void account_launch(Device& d, int ring) {
-  float ms = 0.f;
-  if (hipEventElapsedTime(&ms, d.ev_start[ring], d.ev_stop[ring]) != hipSuccess) ms = 0.f;
-  std::lock_guard<std::mutex> g(d.stats_mu);
-  d.launches++;
-  d.kernel_ms += ms;
 }
 
 // Wait for every in-flight launch, accounting its time.
@@ -148,137 +107,6 @@ int reset_task(Device& d) {
   HIPTRY(hipStreamSynchronize(d.stream));
   store_release(&d.mb->found, 0);
   store_release(&d.mb->abort, 0);
-  return NPOW_OK;
-}
-
-// ---------------------------------------------------------------------------------------
-// First-win search shared by every device of one request.
-struct SharedSearch {
-  std::atomic<int> winner{-1};
-  std::atomic<bool> stop{false};
-  std::atomic<bool> cancelled{false};
-  uint64_t nonce = 0, value = 0;
-  const volatile uint32_t* cancel = nullptr;
-  std::mutex err_mu;
-  int err = NPOW_OK;
-  std::string err_msg;
-  std::atomic<uint64_t> done{0};
-  void set_error(int code, const std::string& m) {
-    std::lock_guard<std::mutex> g(err_mu);
-    if (err == NPOW_OK) {
-      err = code;
-      err_msg = m;
-    }
-    stop = true;
-  }
-};
-
-// Scan this device's stride until a win (here or elsewhere), cancel, or exhaustion.
-int device_search(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t start, uint64_t max_nonces,
-                  SharedSearch& sh) {
-  std::lock_guard<std::mutex> lk(d.mu);
-  HIPTRY(hipSetDevice(d.id));
-  int rc = reset_task(d);
-  if (rc) return rc;
-
-  LaunchArgs a{};
-  fill_uniforms(a, pre);
-  a.threshold = threshold;
-  a.poll_mask = poll_mask();
-  a.cap = 0;
-  const uint64_t chunk = (uint64_t)grid_of(d) * kBlock * g_iters.load();
-  uint64_t issued = 0;
-  int ring = 0, invalid_streak = 0;
-  std::deque<Inflight> q;
-  uint64_t total_done = 0;
-
-  for (;;) {
-    // keep two chunks queued on the stream
-    while (q.size() < 2 && !sh.stop.load(std::memory_order_relaxed) &&
-           (max_nonces == 0 || issued < max_nonces)) {
-      const uint64_t cnt = max_nonces ? std::min(chunk, max_nonces - issued) : chunk;
-      a.base = start + issued;
-      a.count = cnt;
-      rc = launch_chunk(d, Mode::kSearch, a, ring, nullptr);
-      if (rc) return rc;
-      q.push_back({ring, cnt});
-      ring = (ring + 1) % kEventRing;
-      issued += cnt;
-    }
-    // retire finished launches (FIFO)
-    while (!q.empty() && hipEventQuery(d.ev_stop[q.front().ring]) == hipSuccess) {
-      account_launch(d, q.front().ring);
-      q.pop_front();
-    }
-    // a win published by this GPU?
-    if (load_acquire(&d.mb->found)) {
-      const uint64_t n = __atomic_load_n(&d.mb->nonce, __ATOMIC_ACQUIRE);
-      const uint64_t v = __atomic_load_n(&d.mb->value, __ATOMIC_ACQUIRE);
-      const uint64_t cpu_v = host_work_value(pre.m, n);
-      if (cpu_v == v && v >= threshold) {
-        int expected = -1;
-        if (sh.winner.compare_exchange_strong(expected, d.id)) {
-          sh.nonce = n;
-          sh.value = v;
-        }
-        sh.stop = true;
-      } else {
-        // "GPU returned invalid work" -- re-arm and keep searching; give up after 3 in a row.
-        {
-          std::lock_guard<std::mutex> g(d.stats_mu);
-          d.invalid++;
-        }
-        fprintf(stderr, "nanopow: GPU %d returned invalid work %016llx (value %016llx, cpu %016llx)\n", d.id,
-                (unsigned long long)n, (unsigned long long)v, (unsigned long long)cpu_v);
-        rc = drain(d, q);
-        if (rc) return rc;
-        DevState hs;
-        rc = read_state(d, &hs);
-        if (rc) return rc;
-        total_done += hs.done();
-        if (++invalid_streak >= 3) {
-          d.dead = true;
-          sh.done += total_done;
-          return fail(NPOW_ERR_INVALID_WORK,
-                      "GPU " + std::to_string(d.id) +
-                          " returned invalid work 3 consecutive times, abandoning it for this work");
-        }
-        rc = reset_task(d);
-        if (rc) return rc;
-        continue;
-      }
-    }
-    if (!sh.stop.load(std::memory_order_relaxed) && sh.cancel && load_acquire(sh.cancel)) {
-      sh.cancelled = true;
-      sh.stop = true;
-    }
-    if (sh.stop.load(std::memory_order_relaxed)) {
-      store_release(&d.mb->abort, 1);
-      break;
-    }
-    if (q.empty() && max_nonces && issued >= max_nonces) break;  // stride exhausted
-    cpu_relax();
-  }
-  rc = drain(d, q);
-  if (rc) return rc;
-  // a win may have landed in the last chunk of an exhausted stride
-  if (!sh.stop.load() && load_acquire(&d.mb->found)) {
-    const uint64_t n = __atomic_load_n(&d.mb->nonce, __ATOMIC_ACQUIRE);
-    const uint64_t v = __atomic_load_n(&d.mb->value, __ATOMIC_ACQUIRE);
-    if (host_work_value(pre.m, n) == v && v >= threshold) {
-      int expected = -1;
-      if (sh.winner.compare_exchange_strong(expected, d.id)) {
-        sh.nonce = n;
-        sh.value = v;
-      }
-      sh.stop = true;
-    }
-  }
-  DevState hs;
-  rc = read_state(d, &hs);
-  if (rc) return rc;
-  total_done += hs.done();
-  sh.done += total_done;
   return NPOW_OK;
 }
 
@@ -398,15 +226,25 @@ int npow_init(int* n_devices) {
       HIPTRY(hipEventCreate(&d->ev_start[r]));
       HIPTRY(hipEventCreate(&d->ev_stop[r]));
     }
+    if (int rc = pool_device_init(*d)) return rc;
     g_devs.push_back(std::move(d));
   }
   g_init = true;
+  pool_start();
+  static bool exit_hook = false;
+  if (!exit_hook) {
+    // Join the pool's worker threads before static destructors and the HIP runtime's own
+    // exit-time teardown (registered earlier by hipGetDeviceCount, so it runs after this).
+    exit_hook = true;
+    atexit([] { npow_shutdown(); });
+  }
   if (n_devices) *n_devices = (int)g_devs.size();
   return NPOW_OK;
 }
 
 void npow_shutdown(void) {
   std::lock_guard<std::mutex> g(g_mu);
+  if (g_init) pool_stop();
   for (auto& d : g_devs) {
     std::lock_guard<std::mutex> lk(d->mu);
     (void)hipSetDevice(d->id);
@@ -418,6 +256,7 @@ void npow_shutdown(void) {
     (void)hipFree(d->st);
     (void)hipFree(d->d_out);
     (void)hipHostFree(d->mb);
+    pool_device_free(*d);
     (void)hipStreamDestroy(d->stream);
   }
   g_devs.clear();
@@ -431,7 +270,10 @@ uint64_t npow_work_value(const uint8_t root[32], uint64_t nonce) {
 }
 
 int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t blocks_per_cu) {
-  if (iters_per_launch) g_iters = iters_per_launch;
+  if (iters_per_launch) {
+    if (iters_per_launch > 65536) return fail(NPOW_ERR_BAD_ARGUMENT, "iters_per_launch must be <= 65536");
+    g_iters = iters_per_launch;
+  }
   if (poll_interval) g_poll = poll_interval;
   if (blocks_per_cu) {
     if (blocks_per_cu > 32) return fail(NPOW_ERR_BAD_ARGUMENT, "blocks_per_cu must be <= 32");
@@ -469,70 +311,82 @@ int npow_search(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
                 uint64_t* value_out, uint64_t* nonces_done) {
   if (int rc = check_init()) return rc;
   if (!root || !nonce_out) return fail(NPOW_ERR_BAD_ARGUMENT, "root and nonce_out are required");
-  auto devs = select_devices(device_mask);
-  if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable device in device_mask");
-  const RootPrecomp pre = host_precompute(root);
-  SharedSearch sh;
-  sh.cancel = cancel;
-  const uint64_t G = devs.size();
-  const uint64_t spacing = G > 1 ? (~0ull / G) + 1 : 0;  // 2^64 / G (exact for powers of two)
-  run_on_devices(devs, [&](size_t k, Device& d) {
-    int rc = device_search(d, pre, threshold, start + k * spacing, max_nonces_per_device, sh);
-    if (rc) sh.set_error(rc, t_err);
-  });
-  if (nonces_done) *nonces_done = sh.done.load();
-  if (sh.winner.load() >= 0) {
-    *nonce_out = sh.nonce;
-    if (value_out) *value_out = sh.value;
-    return NPOW_OK;
-  }
-  if (sh.err != NPOW_OK) return fail(sh.err, sh.err_msg);
-  if (sh.cancelled.load()) return NPOW_CANCELLED;
-  return NPOW_EXHAUSTED;
+  uint64_t ticket = 0;
+  if (int rc = pool_submit(root, threshold, start, device_mask, max_nonces_per_device, cancel, &ticket)) return rc;
+  return pool_wait(ticket, -1, nonce_out, value_out, nonces_done);
 }
 
 int npow_search_batch(const uint8_t* roots, const uint64_t* thresholds, uint32_t n, uint64_t device_mask,
                       uint64_t max_nonces_per_root, const volatile uint32_t* const* cancel, uint64_t* nonces_out,
                       uint64_t* values_out, int32_t* status_out, uint64_t* nonces_done) {
   if (int rc = check_init()) return rc;
+  if (nonces_done) *nonces_done = 0;
   if (n == 0) return NPOW_OK;
   if (!roots || !thresholds || !nonces_out || !status_out)
     return fail(NPOW_ERR_BAD_ARGUMENT, "roots, thresholds, nonces_out and status_out are required");
-  auto devs = select_devices(device_mask);
-  if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable device in device_mask");
-  std::atomic<uint64_t> done{0};
-  std::mutex err_mu;
+  std::vector<uint64_t> tickets(n, 0);
   int err = NPOW_OK;
   std::string err_msg;
-  run_on_devices(devs, [&](size_t k, Device& d) {
-    for (uint32_t i = (uint32_t)k; i < n; i += (uint32_t)devs.size()) {
-      const RootPrecomp pre = host_precompute(roots + 32 * (size_t)i);
-      SharedSearch sh;
-      sh.cancel = cancel ? cancel[i] : nullptr;
-      // distinct start per root: derived from the root so repeated roots restart identically
-      const uint64_t start = pre.m[0] ^ pre.m[3];
-      int rc = device_search(d, pre, thresholds[i], start, max_nonces_per_root, sh);
-      done += sh.done.load();
-      if (rc) {
-        std::lock_guard<std::mutex> g(err_mu);
-        if (err == NPOW_OK) {
-          err = rc;
-          err_msg = t_err;
-        }
-        status_out[i] = rc;
-        continue;
-      }
-      if (sh.winner.load() >= 0) {
-        nonces_out[i] = sh.nonce;
-        if (values_out) values_out[i] = sh.value;
-        status_out[i] = NPOW_OK;
-      } else {
-        status_out[i] = sh.cancelled.load() ? NPOW_CANCELLED : NPOW_EXHAUSTED;
+  for (uint32_t i = 0; i < n; ++i) {
+    // distinct start per root, derived from the root so repeated roots restart identically
+    const uint8_t* r = roots + 32 * (size_t)i;
+    const uint64_t start = host_load_le64(r) ^ host_load_le64(r + 24);
+    int rc = pool_submit(r, thresholds[i], start, device_mask, max_nonces_per_root, cancel ? cancel[i] : nullptr,
+                         &tickets[i]);
+    if (rc) {
+      status_out[i] = rc;
+      if (err == NPOW_OK) {
+        err = rc;
+        err_msg = last_error();
       }
     }
-  });
-  if (nonces_done) *nonces_done = done.load();
+  }
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (!tickets[i]) continue;
+    uint64_t nonce = 0, value = 0, done = 0;
+    const int rc = pool_wait(tickets[i], -1, &nonce, &value, &done);
+    total += done;
+    status_out[i] = rc;
+    if (rc == NPOW_OK) {
+      nonces_out[i] = nonce;
+      if (values_out) values_out[i] = value;
+    } else if (rc < 0 && err == NPOW_OK) {
+      err = rc;
+      err_msg = last_error();
+    }
+  }
+  if (nonces_done) *nonces_done = total;
   if (err != NPOW_OK) return fail(err, err_msg);
+  return NPOW_OK;
+}
+
+int npow_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
+                uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket) {
+  if (int rc = check_init()) return rc;
+  if (!root || !ticket) return fail(NPOW_ERR_BAD_ARGUMENT, "root and ticket are required");
+  return pool_submit(root, threshold, start, device_mask, max_nonces_per_device, cancel, ticket);
+}
+
+int npow_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce_out, uint64_t* value_out,
+              uint64_t* nonces_done) {
+  if (int rc = check_init()) return rc;
+  return pool_wait(ticket, timeout_us, nonce_out, value_out, nonces_done);
+}
+
+int npow_cancel(uint64_t ticket) {
+  if (int rc = check_init()) return rc;
+  return pool_cancel(ticket);
+}
+
+int npow_pool_config(uint32_t max_active) {
+  if (int rc = check_init()) return rc;
+  return pool_set_max_active(max_active);
+}
+
+int npow_pool_status(uint32_t* queued, uint32_t* active) {
+  if (int rc = check_init()) return rc;
+  pool_counts(queued, active);
   return NPOW_OK;
 }
 

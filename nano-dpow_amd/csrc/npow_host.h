@@ -1,0 +1,97 @@
+// npow_host.h -- host-side state shared by the engine (npow_engine.cpp: devices, sweeps,
+// values, C ABI) and the work pool (npow_pool.cpp: concurrent first-win searches).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <atomic>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/nanopow.h"
+#include "npow_blake2b.h"
+#include "npow_internal.h"
+
+namespace npow {
+
+// Thread-local error message behind npow_last_error().
+int fail(int code, const std::string& msg);
+const std::string& last_error();
+
+#define HIPTRY(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      return ::npow::fail(NPOW_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kEventRing = 4;
+
+struct Device {
+  int id = 0;
+  int cus = 0;
+  hipStream_t stream = nullptr;
+  DevState* st = nullptr;        // device memory (sweep / values tasks)
+  HostMailbox* mb = nullptr;     // pinned host (coherent), host view
+  HostMailbox* mb_dev = nullptr; // device view of the same bytes
+  uint64_t* d_out = nullptr;     // sweep hits / values
+  hipEvent_t ev_start[kEventRing] = {};
+  hipEvent_t ev_stop[kEventRing] = {};
+  std::mutex mu;                 // one task (sweep / values / pool work) per device at a time
+  // work pool (npow_pool.cpp)
+  PoolDevState* pst = nullptr;         // device memory
+  PoolMailbox* pmb = nullptr;          // pinned host (coherent), host view
+  PoolMailbox* pmb_dev = nullptr;      // device view
+  PoolTable* d_tab[kEventRing] = {};   // per in-flight launch
+  PoolTable* h_tab[kEventRing] = {};   // pinned staging
+  unsigned long long* h_done = nullptr;  // pinned read-back of every slot's done shards
+  hipEvent_t ev_done[kMaxSlots] = {};    // the read-back of a retiring slot has landed
+  std::thread worker;
+  // statistics
+  std::mutex stats_mu;
+  uint64_t launches = 0, nonces = 0, invalid = 0;
+  double kernel_ms = 0.0;
+  std::atomic<bool> dead{false};
+};
+
+extern std::vector<std::unique_ptr<Device>> g_devs;
+extern std::atomic<uint32_t> g_iters;          // wave iterations per launch
+extern std::atomic<uint32_t> g_poll;           // host-word poll interval (iterations per wave)
+extern std::atomic<uint32_t> g_blocks_per_cu;  // workgroups per CU
+
+inline int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }
+inline uint32_t poll_mask() {
+  uint32_t p = g_poll.load();
+  uint32_t m = 1;
+  while (m < p) m <<= 1;
+  return m - 1;
+}
+
+inline void store_release(volatile uint32_t* p, uint32_t v) { __atomic_store_n((uint32_t*)p, v, __ATOMIC_RELEASE); }
+inline uint32_t load_acquire(const volatile uint32_t* p) { return __atomic_load_n((const uint32_t*)p, __ATOMIC_ACQUIRE); }
+inline void cpu_relax() {
+#if defined(__x86_64__)
+  __builtin_ia32_pause();
+#endif
+}
+
+// Devices selected by a mask (0 = all), excluding dead ones.
+std::vector<Device*> select_devices(uint64_t mask);
+// Per-launch event accounting (kernel time by HIP events on the launch's own stream).
+void account_launch(Device& d, int ring);
+
+// ---- work pool (npow_pool.cpp) ----------------------------------------------------------------
+int pool_device_init(Device& d);     // allocate pool buffers of one device
+void pool_device_free(Device& d);
+void pool_start();                   // start one worker thread per device
+void pool_stop();                    // stop and join the workers (pending jobs end with an error)
+int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
+                uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket);
+int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done);
+int pool_cancel(uint64_t ticket);
+int pool_set_max_active(uint32_t n);
+void pool_counts(uint32_t* queued, uint32_t* active);
+
+}  // namespace npow

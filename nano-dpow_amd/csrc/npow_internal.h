@@ -1,5 +1,6 @@
 // npow_internal.h -- structures shared by the gfx950 kernels and the host engine.
 #pragma once
+#include <stddef.h>
 #include <stdint.h>
 #include <hip/hip_runtime.h>
 
@@ -10,7 +11,7 @@ namespace npow {
 
 constexpr int kBlock = 256;  // lanes per workgroup (4 waves of 64)
 
-enum class Mode : int { kSearch = 0, kSweep = 1, kValues = 2 };
+enum class Mode : int { kSweep = 1, kValues = 2 };  // npow_task_kernel (first-win search: npow_pool_kernel)
 
 // Kernel arguments, passed by value: the kernarg segment lands in SGPRs, so the
 // root-derived uniforms and the threshold cost no memory traffic per nonce
@@ -32,7 +33,7 @@ constexpr int kDoneShards = 256;
 struct DevState {
   union {
     struct {
-      uint32_t found;       // first-win slot: 0 -> 1 by atomicCAS (search)
+      uint32_t found;       // unused (first-win search lives in the pool); always 0
       uint32_t abort;       // host abort relayed by the wave that saw it
     };
     uint64_t stop;          // both, read by every wave with one 8-byte load
@@ -65,9 +66,69 @@ struct alignas(64) HostMailbox {
   uint8_t pad2[60];
 };
 
+// ---- Work pool: many roots searched by one launch (npow_pool_kernel) -----------------------
+// Each device keeps up to kMaxSlots live jobs in "slots".  Every launch reads a table of
+// the live entries (device memory, one copy per in-flight launch); wave w starts on entry
+// w % n.  A slot is identified per job by a generation number `gen` (unique, > 0): a slot
+// is dead for generation g once PoolDevState::slot[s].dead >= g (set by its winner with
+// atomicMax, or relayed from the host kill word), so a slot can be reused for a new job
+// with a larger gen without clearing any device memory.
+constexpr int kMaxSlots = 64;
+constexpr int kPoolDoneShards = 32;
+
+// Nonce-index mapping of one entry (the launch's region is [base, base + count)):
+//  * unbounded (search until won/cancelled): index = (it * W + w) * 64 + lane, W = grid
+//    waves -- every (iteration, wave) pair is distinct, so waves that migrate here from a
+//    dead entry hash fresh nonces; the region spans W * iters * 64 nonces (holes allowed);
+//  * bounded (max_nonces set; must cover its range exactly once): only the entry's own
+//    waves (w % n == e, rank j = w / n, k_e of them) run it, index = (it * k_e + j) * 64 +
+//    lane, dense over [0, count) with count <= k_e * iters * 64; migrants never enter it.
+struct PoolEntry {
+  uint64_t u[NPOW_ASM_N_UNIFORMS];  // nonce-independent intermediates of the root
+  uint64_t threshold;
+  uint64_t base;
+  uint64_t count;
+  uint64_t gen;
+  uint32_t slot;     // device slot index (PoolDevState / PoolMailbox arrays)
+  uint32_t bounded;  // 1: dense mapping over the entry's own waves, no migrants
+};
+struct PoolTable {
+  uint32_t n;          // entries in use (1..kMaxSlots)
+  uint32_t poll_mask;  // a wave reads the host kill word when ((it + w) & poll_mask) == 0
+  uint32_t iters;      // wave iterations of this launch
+  uint32_t pad[13];
+  PoolEntry e[kMaxSlots];
+};
+inline size_t pool_table_bytes(uint32_t n) { return offsetof(PoolTable, e) + (size_t)n * sizeof(PoolEntry); }
+
+struct PoolSlotWord {
+  unsigned long long dead;  // highest generation known dead in this slot
+  uint8_t pad[56];
+};
+struct PoolDevState {
+  PoolSlotWord slot[kMaxSlots];
+  unsigned long long done[kMaxSlots][kPoolDoneShards * 8];  // nonces hashed, sharded over 64-B lines
+};
+
+// Pinned host-coherent mailbox of the pool: one win record per slot (the winner stores
+// nonce and value, then releases gen) and one kill word per slot the host raises.
+struct alignas(64) PoolWin {
+  uint64_t gen;
+  uint64_t nonce;
+  uint64_t value;
+  uint8_t pad[40];
+};
+struct PoolMailbox {
+  PoolWin win[kMaxSlots];
+  uint64_t kill[kMaxSlots];  // kill[s] = gen: the job in slot s (that generation) must stop
+};
+
 // Launchers (defined in npow_kernel.hip).
 hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs& a, DevState* st,
                        HostMailbox* mb, uint64_t* out);
+// bounded: the table holds a bounded entry (selects the kernel variant with per-lane range tests)
+hipError_t launch_pool(int grid, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
+                       PoolMailbox* mb);
 // Fill a.u[] for one root (host).
 inline void fill_uniforms(LaunchArgs& a, const RootPrecomp& pre) { npow_asm_uniforms(pre.m, a.u); }
 

@@ -18,12 +18,14 @@
 //    `v_alignbit_b32` each.
 //  * Grid-stride loop over the launch's nonce range; the hit test is a wave
 //    ballot, so a wave leaves the fast path only when one of its 64 lanes wins.
-//  * Search mode: first win by atomicCAS on a device slot, published to a
-//    host-coherent mailbox with system-scope stores; every wave polls the
-//    device slot each iteration (agent-scope load, L2) and the host abort
-//    word every poll_mask+1 iterations (system-scope load).
-//  * Sweep mode: every hit appended through an atomic counter (order-free;
-//    the host sorts).  Values mode: writes every value (parity tests).
+//  * First-win search (npow_pool_kernel): every live job of the device's work
+//    pool in one launch; first win per job by atomicMax on its slot's dead word,
+//    published to a host-coherent mailbox with system-scope stores; every wave
+//    polls its slot's dead word each iteration (agent-scope load, L2) and the
+//    host kill word every poll_mask+1 iterations (system-scope load).
+//  * Sweep (npow_task_kernel<kSweep>): every hit appended through an atomic
+//    counter (order-free; the host sorts).  Values mode: writes every value
+//    (parity tests).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -159,26 +161,9 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
     } else {
       const bool hit = in_range && value >= a.threshold;
       const uint64_t hits = __ballot(hit);
-      if (__builtin_expect(hits != 0, 0)) {
-        if constexpr (MODE == Mode::kSearch) {
-          const int w = __builtin_ctzll(hits);
-          const uint64_t wn = readlane64(nonce, w), wv = readlane64(value, w);
-          if (lane == 0) {
-            if (atomicCAS(&st->found, 0u, 1u) == 0u) {
-              st->nonce = wn;
-              st->value = wv;
-              __hip_atomic_store(&mb->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              __hip_atomic_store(&mb->value, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              __hip_atomic_store(&mb->found, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-            }
-          }
-          break;
-        } else {  // sweep: append every hit
-          if (hit) {
-            const uint32_t slot = atomicAdd(&st->n_hits, 1u);
-            if (slot < a.cap) out[slot] = nonce;
-          }
-        }
+      if (__builtin_expect(hits != 0, 0) && hit) {  // sweep: append every hit
+        const uint32_t slot = atomicAdd(&st->n_hits, 1u);
+        if (slot < a.cap) out[slot] = nonce;
       }
       if (__builtin_amdgcn_readfirstlane(host_abort)) {
         if (lane == 0) __hip_atomic_store(&st->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -188,6 +173,146 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
     }
   }
   if (lane == 0 && done) atomicAdd(&st->done_shard[(blockIdx.x % kDoneShards) * 8], (unsigned long long)done);
+}
+
+// ---- Work pool: many roots per launch ------------------------------------------------------
+// One launch searches every live entry of the device's table (up to kMaxSlots jobs: the
+// DPoW burst, many work_generate requests in flight).  Wave w starts on entry w % n with
+// the entry's uniforms in SGPRs; when its entry dies (won here, won on another GPU,
+// cancelled, or its bounded range is used up) the wave moves to the next live unbounded
+// entry instead of idling for the rest of the launch.  Index mapping: PoolEntry comment in
+// npow_internal.h.  With one entry this is the plain first-win search.
+struct PoolCursor {
+  uint64_t u[NPOW_ASM_N_UNIFORMS];
+  uint64_t threshold, base, gen;
+  uint32_t slot;
+  uint32_t K, j;      // block index b = it * K + j; nonce = base + b * 64 + lane
+  uint32_t it_end;    // the wave runs the entry while it < it_end
+  uint32_t last_b;    // bounded: index of the entry's last block ...
+  uint32_t tail;      // ... and its lanes in range (64 = full)
+};
+
+// Load entry `pe` into the cursor for wave w.  own: the entry's own waves (w % n == e) --
+// bounded entries are dense over their own waves; everything else uses (it, w) directly.
+__device__ __forceinline__ void pool_load(const PoolEntry* __restrict__ pe, PoolCursor& c, bool own, uint32_t w,
+                                          uint32_t W, uint32_t n, uint32_t e, uint32_t iters) {
+#pragma unroll
+  for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) c.u[i] = pe->u[i];
+  c.threshold = pe->threshold;
+  c.base = pe->base;
+  c.gen = pe->gen;
+  c.slot = pe->slot;
+  if (pe->bounded) {
+    // own waves only (migrants never pick a bounded entry); count <= K * iters * 64 < 2^32 * 64
+    c.K = W / n + (e < W % n ? 1u : 0u);
+    c.j = w / n;
+    const uint32_t blocks = (uint32_t)((pe->count + 63) / 64);  // <= K * iters < 2^31
+    c.it_end = blocks > c.j ? (blocks - c.j + c.K - 1) / c.K : 0u;
+    c.last_b = blocks - 1u;
+    c.tail = (uint32_t)(pe->count - (uint64_t)(blocks - 1u) * 64);
+  } else {
+    c.K = W;
+    c.j = w;
+    c.it_end = iters;
+    c.last_b = 0xffffffffu;
+    c.tail = 64;
+  }
+  (void)own;
+}
+
+__device__ __forceinline__ uint64_t load_dead(PoolDevState* st, uint32_t slot) {
+  return __hip_atomic_load(&st->slot[slot].dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// BOUNDED: the table holds at least one bounded entry (partial last blocks need a per-lane
+// range test); the plain search (every entry unbounded) compiles without it.
+template <bool BOUNDED>
+__global__ __launch_bounds__(kBlock) void npow_pool_kernel(const PoolTable* __restrict__ tab,
+                                                           PoolDevState* __restrict__ st,
+                                                           PoolMailbox* __restrict__ mb) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t w = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
+  const uint32_t W = gridDim.x * (kBlock / 64);
+  const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask;
+  unsigned long long* const done_base = &st->done[0][(blockIdx.x % kPoolDoneShards) * 8];
+
+  uint32_t e = w % n;
+  PoolCursor c;
+  pool_load(&tab->e[e], c, true, w, W, n, e, iters);
+
+  uint32_t it = 0;
+  for (;;) {
+    uint32_t done = 0;  // nonces this wave hashed for the current entry (<= iters * 64)
+    while (it < c.it_end) {
+      // polls: the slot's dead word every iteration (agent scope, L2); the pinned host
+      // kill word by one wave in poll_mask+1 (a PCIe read).  Consumed after the hash.
+#ifndef NPOW_POOL_POLL
+#define NPOW_POOL_POLL 3
+#endif
+      const uint64_t dead = (NPOW_POOL_POLL & 1) ? load_dead(st, c.slot) : 0;
+      uint64_t kill = 0;
+      if ((NPOW_POOL_POLL & 2) && ((it + w) & poll_mask) == 0)
+        kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+
+      const uint32_t b = it * c.K + c.j;  // < 2^31: the entry's blocks of this launch
+      const uint64_t nonce = c.base + ((uint64_t)b << 6) + lane;
+      const uint64_t value = npow_asm_work_value(nonce, c.u);
+      ++it;
+      bool hit = value >= c.threshold;
+      if constexpr (BOUNDED) {
+        const uint32_t in_lanes = b == c.last_b ? c.tail : 64u;
+        hit = hit && lane < in_lanes;
+        done += in_lanes;
+      } else {
+        done += 64;
+      }
+      const uint64_t hits = __ballot(hit);
+      if (__builtin_expect(hits != 0, 0)) {
+        const int wl = __builtin_ctzll(hits);
+        const uint64_t wn = readlane64(nonce, wl), wv = readlane64(value, wl);
+        if (lane == 0) {
+          if (atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen) < c.gen) {  // first win
+            PoolWin* pw = &mb->win[c.slot];
+            __hip_atomic_store(&pw->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&pw->value, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&pw->gen, c.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+        break;
+      }
+      if (readlane64(kill, 0) == c.gen) {  // generations only grow: == is "this job"
+        if (lane == 0) atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen);  // relay
+        break;
+      }
+      if (readlane64(dead, 0) == c.gen) break;
+    }
+    if (lane == 0 && done) atomicAdd(done_base + (size_t)c.slot * (kPoolDoneShards * 8), (unsigned long long)done);
+    if (it >= iters) break;
+    // the entry died or its bounded range is used up: next live unbounded entry (cyclic
+    // from e + 1); none left -> the wave is finished
+    uint32_t next = n;
+    for (uint32_t k = 1; k < n; ++k) {
+      uint32_t e2 = e + k;
+      if (e2 >= n) e2 -= n;
+      const PoolEntry* pe = &tab->e[e2];
+      if (pe->bounded) continue;
+      if (load_dead(st, pe->slot) >= pe->gen) continue;
+      next = e2;
+      break;
+    }
+    if (next == n) break;
+    e = next;
+    pool_load(&tab->e[e], c, false, w, W, n, e, iters);
+  }
+}
+
+hipError_t launch_pool(int grid, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
+                       PoolMailbox* mb) {
+  if (bounded)
+    npow_pool_kernel<true><<<grid, kBlock, 0, stream>>>(tab, st, mb);
+  else
+    npow_pool_kernel<false><<<grid, kBlock, 0, stream>>>(tab, st, mb);
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(kBlock) void npow_pairs_kernel(const uint64_t* __restrict__ roots_words,
@@ -204,9 +329,6 @@ __global__ __launch_bounds__(kBlock) void npow_pairs_kernel(const uint64_t* __re
 hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs& a, DevState* st,
                        HostMailbox* mb, uint64_t* out) {
   switch (mode) {
-    case Mode::kSearch:
-      npow_task_kernel<Mode::kSearch><<<grid, kBlock, 0, stream>>>(a, st, mb, out);
-      break;
     case Mode::kSweep:
       npow_task_kernel<Mode::kSweep><<<grid, kBlock, 0, stream>>>(a, st, mb, out);
       break;

@@ -1,0 +1,624 @@
+// npow_pool.cpp -- the work pool of libnanopow.so: every first-win search (npow_search,
+// npow_search_batch, npow_submit) is a job; up to max_active jobs are searched at once,
+// all of them by ONE kernel launch per device (npow_pool_kernel), each on a disjoint
+// per-device stride of its nonce space.
+//
+// Replaces the request queue and GPU loop of the reference work server
+// (client/bin/windows/nano-work-server.exe, Rust source not vendored; behaviour from its
+// strings): requests queue FIFO (@1681064 `--shuffle` is the server's choice of order),
+// every GPU scans nonce chunks for the queued root, each GPU result is re-validated on the
+// CPU ("GPU returned invalid work", @1669040; a device is abandoned for the work after 3
+// in a row, @1669144), and work_cancel ends the request with "Cancelled" (@1673856).
+// The reference serves ONE root at a time; a DPoW burst (many work_generate requests in
+// flight, client/work_handler.py:83-125 per client) is served here by keeping up to
+// kMaxSlots roots live in every launch, so a root that is won mid-launch costs nothing:
+// its waves move on to the other live roots (npow_kernel.hip, npow_pool_kernel).
+//
+// Threads: one persistent worker per device (started by npow_init) owns the device's
+// stream, its slot table and two launches in flight; callers block in pool_wait.  The
+// only cross-device datum is a job's outcome: the first device whose winner passes CPU
+// re-validation decides the job, the others raise their slot's kill word (pinned host
+// memory that the waves poll) and retire it.  No collective, no device-to-device traffic.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "npow_host.h"
+
+namespace npow {
+namespace {
+
+constexpr int kPending = 100;  // job status before it is decided
+
+struct Job {
+  uint64_t ticket = 0;
+  RootPrecomp pre{};
+  uint64_t u[NPOW_ASM_N_UNIFORMS] = {};
+  uint64_t threshold = 0, start = 0, max_per_dev = 0, spacing = 0;
+  const volatile uint32_t* cancel = nullptr;
+  std::vector<int> devs;  // device ids; the k-th scans from start + k * spacing
+  // guarded by g_pool.mu
+  std::vector<uint64_t> issued;     // per device k: nonces of its stride handed to launches
+  std::vector<uint8_t> on_dev;      // per device k: a slot holds the job
+  std::vector<uint8_t> dev_done;    // per device k: finished with the job
+  std::vector<int> invalid_streak;  // per device k
+  int pending_devs = 0;
+  bool admitted = false;
+  std::atomic<bool> finished{false};  // written under g_pool.mu; waiters may spin on it
+  int status = kPending;
+  uint64_t nonce = 0, value = 0, done = 0;
+  std::string err;
+  // lock-free flags the workers poll
+  std::atomic<bool> decided{false};
+  std::atomic<bool> cancel_req{false};
+
+  bool cancel_seen() const { return cancel_req.load(std::memory_order_relaxed) || (cancel && load_acquire(cancel)); }
+};
+using JobP = std::shared_ptr<Job>;
+
+struct Pool {
+  std::mutex mu;
+  std::condition_variable cv_work;  // workers: new admissions / shutdown
+  std::condition_variable cv_done;  // waiters: a job finished
+  std::deque<JobP> waiting;
+  std::vector<JobP> active;
+  std::unordered_map<uint64_t, JobP> tickets;
+  uint64_t next_ticket = 1;
+  uint32_t max_active = kMaxSlots;
+  bool running = false;
+  std::atomic<uint64_t> version{0};  // bumped whenever `active` gains a job
+} g_pool;
+
+std::atomic<uint64_t> g_gen{0};
+
+// -- job state transitions (caller holds g_pool.mu) ------------------------------------------
+void decide_locked(Job& j, int status, uint64_t nonce = 0, uint64_t value = 0) {
+  if (j.status != kPending) return;
+  j.status = status;
+  j.nonce = nonce;
+  j.value = value;
+  j.decided = true;
+}
+
+void admit_locked() {
+  bool added = false;
+  while (g_pool.active.size() < g_pool.max_active && !g_pool.waiting.empty()) {
+    JobP j = g_pool.waiting.front();
+    g_pool.waiting.pop_front();
+    j->admitted = true;
+    g_pool.active.push_back(j);
+    added = true;
+  }
+  if (added) {
+    g_pool.version.fetch_add(1);
+    g_pool.cv_work.notify_all();
+  }
+}
+
+void finish_locked(const JobP& j) {
+  if (j->finished) return;
+  if (j->status == kPending) {
+    if (j->cancel_seen()) j->status = NPOW_CANCELLED;
+    else if (!j->err.empty()) j->status = NPOW_ERR_HIP;
+    else j->status = NPOW_EXHAUSTED;
+    j->decided = true;
+  }
+  j->finished = true;
+  auto it = std::find(g_pool.active.begin(), g_pool.active.end(), j);
+  if (it != g_pool.active.end()) g_pool.active.erase(it);
+  auto wt = std::find(g_pool.waiting.begin(), g_pool.waiting.end(), j);
+  if (wt != g_pool.waiting.end()) g_pool.waiting.erase(wt);
+  admit_locked();
+  g_pool.cv_done.notify_all();
+}
+
+// Device k of job j is finished with it (retired, exhausted, or the device failed).
+void device_done_locked(const JobP& j, size_t k) {
+  if (j->dev_done[k]) return;
+  j->dev_done[k] = 1;
+  j->on_dev[k] = 0;
+  if (--j->pending_devs == 0) finish_locked(j);
+}
+
+// -- one device's worker ------------------------------------------------------------------------
+enum class SlotState { kFree, kActive, kDraining };
+
+struct Slot {
+  SlotState state = SlotState::kFree;
+  JobP job;
+  size_t k = 0;            // the device's index within job->devs
+  uint64_t gen = 0;
+  uint64_t baseline = 0;   // done counter of this slot index at its last retirement
+  bool win_seen = false;
+  bool requeue = false;    // invalid GPU result: hand the job back to this device after retiring
+  bool no_more = false;    // bounded range fully issued
+  bool readback = false;   // done-shard read-back queued (ev_done[slot] marks it)
+};
+
+struct PoolInflight {
+  uint64_t seq;
+  int ring;
+};
+
+class Worker {
+ public:
+  explicit Worker(Device& d) : d_(d) {}
+  void run();
+
+ private:
+  Device& d_;
+  Slot slots_[kMaxSlots];
+  std::deque<PoolInflight> q_;
+  uint64_t seq_ = 0;  // launches issued by this worker
+  uint64_t seen_version_ = ~0ull;
+  int ring_ = 0;
+  std::unique_lock<std::mutex> dev_lock_{d_.mu, std::defer_lock};
+
+  bool busy() const {
+    if (!q_.empty()) return true;
+    for (const Slot& s : slots_)
+      if (s.state != SlotState::kFree) return true;
+    return false;
+  }
+  void adopt();
+  void handle_win(int s);
+  bool win_published(int s) const;
+  void check_slots();
+  int launch();
+  int queue_readbacks();
+  int retire();
+  void fail_all(const std::string& msg);
+  int step();
+};
+
+int index_in(const Job& j, int dev) {
+  for (size_t k = 0; k < j.devs.size(); ++k)
+    if (j.devs[k] == dev) return (int)k;
+  return -1;
+}
+
+// Needs (under g_pool.mu): some active job wants this device.
+bool wants_device_locked(int dev) {
+  for (const JobP& j : g_pool.active) {
+    const int k = index_in(*j, dev);
+    if (k >= 0 && !j->on_dev[k] && !j->dev_done[k]) return true;
+  }
+  return false;
+}
+
+void Worker::adopt() {
+  const uint64_t v = g_pool.version.load();
+  if (v == seen_version_) return;
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  seen_version_ = g_pool.version.load();
+  for (const JobP& j : std::vector<JobP>(g_pool.active)) {  // copy: device_done_locked may erase
+    const int k = index_in(*j, d_.id);
+    if (k < 0 || j->on_dev[k] || j->dev_done[k]) continue;
+    if (j->decided) {  // decided before this device got to it
+      device_done_locked(j, k);
+      continue;
+    }
+    int s = 0;
+    while (s < kMaxSlots && slots_[s].state != SlotState::kFree) ++s;
+    if (s == kMaxSlots) {  // cannot happen while max_active <= kMaxSlots; retry later
+      seen_version_ = ~0ull;
+      break;
+    }
+    Slot& sl = slots_[s];
+    sl.state = SlotState::kActive;
+    sl.job = j;
+    sl.k = (size_t)k;
+    sl.gen = ++g_gen;
+    sl.win_seen = sl.requeue = sl.no_more = sl.readback = false;
+    j->on_dev[k] = 1;
+  }
+}
+
+// A win published for slot s (this generation): CPU re-validation decides the job.
+void Worker::handle_win(int s) {
+  Slot& sl = slots_[s];
+  Job& j = *sl.job;
+  PoolWin& pw = d_.pmb->win[s];
+  sl.win_seen = true;
+  const uint64_t n = __atomic_load_n(&pw.nonce, __ATOMIC_RELAXED);
+  const uint64_t v = __atomic_load_n(&pw.value, __ATOMIC_RELAXED);
+  const uint64_t cpu_v = host_work_value(j.pre.m, n);
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  if (cpu_v == v && v >= j.threshold) {
+    j.invalid_streak[sl.k] = 0;
+    decide_locked(j, NPOW_OK, n, v);
+  } else {
+    // "GPU returned invalid work": re-arm this device for the job after the slot retires
+    {
+      std::lock_guard<std::mutex> sg(d_.stats_mu);
+      d_.invalid++;
+    }
+    fprintf(stderr, "nanopow: GPU %d returned invalid work %016llx (value %016llx, cpu %016llx)\n", d_.id,
+            (unsigned long long)n, (unsigned long long)v, (unsigned long long)cpu_v);
+    if (++j.invalid_streak[sl.k] >= 3)
+      j.err = "GPU " + std::to_string(d_.id) + " returned invalid work 3 consecutive times, abandoning it for this work";
+    else
+      sl.requeue = true;
+  }
+  sl.state = SlotState::kDraining;  // the winning wave already marked the slot dead on the device
+}
+
+bool Worker::win_published(int s) const {
+  const Slot& sl = slots_[s];
+  return !sl.win_seen && __atomic_load_n(&d_.pmb->win[s].gen, __ATOMIC_ACQUIRE) == sl.gen;
+}
+
+void Worker::check_slots() {
+  for (int s = 0; s < kMaxSlots; ++s) {
+    Slot& sl = slots_[s];
+    if (sl.state == SlotState::kFree) continue;
+    if (win_published(s)) {
+      handle_win(s);
+      continue;
+    }
+    if (sl.state != SlotState::kActive) continue;
+    Job& j = *sl.job;
+    if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {
+      if (!j.decided.load()) {
+        std::lock_guard<std::mutex> g(g_pool.mu);
+        j.cancel_req = true;
+        decide_locked(j, NPOW_CANCELLED);
+      }
+      __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);  // in-flight waves stop
+      sl.state = SlotState::kDraining;
+    } else if (sl.no_more) {
+      sl.state = SlotState::kDraining;
+    }
+  }
+}
+
+int Worker::launch() {
+  if (q_.size() >= 2) return NPOW_OK;
+  const uint32_t iters = g_iters.load();
+  const uint32_t W = (uint32_t)grid_of(d_) * (kBlock / 64);
+  PoolTable& t = *d_.h_tab[ring_];
+  uint32_t n = 0;
+  bool bounded = false;
+  int idx[kMaxSlots];
+  for (int s = 0; s < kMaxSlots; ++s)
+    if (slots_[s].state == SlotState::kActive && !slots_[s].no_more) idx[n++] = s;
+  if (n == 0) return NPOW_OK;
+  t.n = n;
+  t.poll_mask = poll_mask();
+  t.iters = iters;
+  ++seq_;
+  {
+    std::lock_guard<std::mutex> g(g_pool.mu);  // issued[] is shared with other workers' reads
+    for (uint32_t e = 0; e < n; ++e) {
+      Slot& sl = slots_[idx[e]];
+      Job& j = *sl.job;
+      PoolEntry& pe = t.e[e];
+      memcpy(pe.u, j.u, sizeof(pe.u));
+      pe.threshold = j.threshold;
+      pe.gen = sl.gen;
+      pe.slot = (uint32_t)idx[e];
+      uint64_t& issued = j.issued[sl.k];
+      pe.base = j.start + sl.k * j.spacing + issued;
+      if (j.max_per_dev) {
+        const uint64_t own = (uint64_t)(W / n + (e < W % n ? 1u : 0u)) * iters * 64;
+        pe.count = std::min(own, j.max_per_dev - issued);
+        pe.bounded = 1;
+        bounded = true;
+      } else {
+        pe.count = (uint64_t)W * iters * 64;
+        pe.bounded = 0;
+      }
+      issued += pe.count;
+      if (j.max_per_dev && issued >= j.max_per_dev) sl.no_more = true;
+    }
+  }
+  const int r = ring_;
+  ring_ = (ring_ + 1) % kEventRing;
+  const size_t bytes = pool_table_bytes(n);
+  // The table goes up in stream order right before its launch.  (Uploading it on a second
+  // stream beside the running launch, joined by an event, cost 1.5-2 % of kernel throughput:
+  // the copy is a blit kernel that competes with the running launch.)
+  HIPTRY(hipMemcpyAsync(d_.d_tab[r], d_.h_tab[r], bytes, hipMemcpyHostToDevice, d_.stream));
+  HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
+  HIPTRY(launch_pool(grid_of(d_), d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
+  HIPTRY(hipEventRecord(d_.ev_stop[r], d_.stream));
+  q_.push_back({seq_, r});
+  return NPOW_OK;
+}
+
+// Slots that just left the tables: read their done shards back in stream order, behind every
+// launch that still holds them (later launches do not), and note when that copy lands.
+int Worker::queue_readbacks() {
+  constexpr size_t row = kPoolDoneShards * 8;
+  for (int s = 0; s < kMaxSlots; ++s) {
+    Slot& sl = slots_[s];
+    if (sl.state != SlotState::kDraining || sl.readback) continue;
+    HIPTRY(hipMemcpyAsync(d_.h_done + (size_t)s * row, &d_.pst->done[s][0], row * sizeof(unsigned long long),
+                          hipMemcpyDeviceToHost, d_.stream));
+    HIPTRY(hipEventRecord(d_.ev_done[s], d_.stream));
+    sl.readback = true;
+  }
+  return NPOW_OK;
+}
+
+int Worker::retire() {
+  while (!q_.empty()) {
+    const hipError_t e = hipEventQuery(d_.ev_stop[q_.front().ring]);
+    if (e == hipErrorNotReady) break;
+    if (e != hipSuccess) return fail(NPOW_ERR_HIP, std::string("pool launch: ") + hipGetErrorString(e));
+    account_launch(d_, q_.front().ring);
+    q_.pop_front();
+  }
+  constexpr size_t row = kPoolDoneShards * 8;
+  for (int s = 0; s < kMaxSlots; ++s) {
+    Slot& sl = slots_[s];
+    if (sl.state != SlotState::kDraining || !sl.readback) continue;
+    const hipError_t e = hipEventQuery(d_.ev_done[s]);
+    if (e == hipErrorNotReady) continue;
+    if (e != hipSuccess) return fail(NPOW_ERR_HIP, std::string("pool read-back: ") + hipGetErrorString(e));
+    // every launch that held the slot has completed: its done shards are final
+    uint64_t sum = 0;
+    for (int i = 0; i < kPoolDoneShards; ++i) sum += d_.h_done[(size_t)s * row + i * 8];
+    const uint64_t delta = sum - sl.baseline;
+    sl.baseline = sum;
+    {
+      std::lock_guard<std::mutex> sg(d_.stats_mu);
+      d_.nonces += delta;
+    }
+    if (win_published(s)) handle_win(s);  // published by the last launch, not yet seen
+    {
+      std::lock_guard<std::mutex> g(g_pool.mu);
+      Job& j = *sl.job;
+      j.done += delta;
+      if (sl.requeue && !j.decided && j.err.empty()) {
+        j.on_dev[sl.k] = 0;  // adopt() picks it up again with a fresh generation
+        g_pool.version.fetch_add(1);
+      } else {
+        device_done_locked(sl.job, sl.k);
+      }
+    }
+    sl.job.reset();
+    sl.state = SlotState::kFree;
+  }
+  return NPOW_OK;
+}
+
+void Worker::fail_all(const std::string& msg) {
+  d_.dead = true;
+  fprintf(stderr, "nanopow: device %d failed: %s\n", d_.id, msg.c_str());
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  for (Slot& sl : slots_) {
+    if (sl.state == SlotState::kFree) continue;
+    if (sl.job->err.empty()) sl.job->err = msg;
+    device_done_locked(sl.job, sl.k);
+    sl.job.reset();
+    sl.state = SlotState::kFree;
+  }
+  q_.clear();
+}
+
+int Worker::step() {
+  adopt();
+  check_slots();
+  if (int rc = queue_readbacks()) return rc;  // before the next launch: it no longer holds them
+  if (int rc = launch()) return rc;
+  if (int rc = retire()) return rc;
+  return NPOW_OK;
+}
+
+void Worker::run() {
+  if (hipSetDevice(d_.id) != hipSuccess) d_.dead = true;
+  for (;;) {
+    if (d_.dead) {
+      // a failed device only releases the jobs that name it
+      std::unique_lock<std::mutex> lk(g_pool.mu);
+      for (const JobP& j : std::vector<JobP>(g_pool.active)) {
+        const int k = index_in(*j, d_.id);
+        if (k >= 0 && !j->dev_done[k]) {
+          if (j->err.empty()) j->err = "device " + std::to_string(d_.id) + " failed";
+          device_done_locked(j, (size_t)k);
+        }
+      }
+      if (!g_pool.running) return;
+      g_pool.cv_work.wait(lk);
+      continue;
+    }
+    if (!busy()) adopt();  // jobs admitted since the last look
+    if (!busy()) {
+      if (dev_lock_.owns_lock()) dev_lock_.unlock();
+      std::unique_lock<std::mutex> lk(g_pool.mu);
+      g_pool.cv_work.wait(lk, [&] { return !g_pool.running || wants_device_locked(d_.id); });
+      if (!g_pool.running) return;
+      continue;
+    }
+    if (!dev_lock_.owns_lock()) dev_lock_.lock();  // waits behind a sweep / values task on this device
+    if (step() != NPOW_OK) {
+      fail_all(last_error());
+      if (dev_lock_.owns_lock()) dev_lock_.unlock();
+      continue;
+    }
+    cpu_relax();
+  }
+}
+
+}  // namespace
+
+// -- device resources -----------------------------------------------------------------------------
+int pool_device_init(Device& d) {
+  HIPTRY(hipMalloc(&d.pst, sizeof(PoolDevState)));
+  HIPTRY(hipMemset(d.pst, 0, sizeof(PoolDevState)));
+  void* mb = nullptr;
+  HIPTRY(hipHostMalloc(&mb, sizeof(PoolMailbox), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+  memset(mb, 0, sizeof(PoolMailbox));
+  d.pmb = (PoolMailbox*)mb;
+  void* mbd = nullptr;
+  HIPTRY(hipHostGetDevicePointer(&mbd, mb, 0));
+  d.pmb_dev = (PoolMailbox*)mbd;
+  for (int r = 0; r < kEventRing; ++r) {
+    HIPTRY(hipMalloc(&d.d_tab[r], sizeof(PoolTable)));
+    void* h = nullptr;
+    HIPTRY(hipHostMalloc(&h, sizeof(PoolTable), hipHostMallocDefault));
+    memset(h, 0, sizeof(PoolTable));
+    d.h_tab[r] = (PoolTable*)h;
+  }
+  void* hd = nullptr;
+  HIPTRY(hipHostMalloc(&hd, (size_t)kMaxSlots * kPoolDoneShards * 8 * sizeof(unsigned long long), hipHostMallocDefault));
+  d.h_done = (unsigned long long*)hd;
+  for (int s = 0; s < kMaxSlots; ++s) HIPTRY(hipEventCreateWithFlags(&d.ev_done[s], hipEventDisableTiming));
+  return NPOW_OK;
+}
+
+void pool_device_free(Device& d) {
+  (void)hipFree(d.pst);
+  (void)hipHostFree(d.pmb);
+  for (int r = 0; r < kEventRing; ++r) {
+    (void)hipFree(d.d_tab[r]);
+    (void)hipHostFree(d.h_tab[r]);
+  }
+  (void)hipHostFree(d.h_done);
+  for (int s = 0; s < kMaxSlots; ++s) (void)hipEventDestroy(d.ev_done[s]);
+}
+
+void pool_start() {
+  {
+    std::lock_guard<std::mutex> g(g_pool.mu);
+    g_pool.running = true;
+  }
+  for (auto& dp : g_devs) {
+    Device* d = dp.get();
+    d->worker = std::thread([d] {
+      Worker w(*d);
+      w.run();
+    });
+  }
+}
+
+void pool_stop() {
+  std::vector<JobP> pending;
+  {
+    std::lock_guard<std::mutex> g(g_pool.mu);
+    g_pool.running = false;
+    for (const JobP& j : g_pool.active) j->cancel_req = true;
+    g_pool.cv_work.notify_all();
+  }
+  for (auto& d : g_devs)
+    if (d->worker.joinable()) d->worker.join();
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  for (auto& kv : g_pool.tickets) {
+    const JobP& j = kv.second;
+    if (!j->finished) {
+      if (j->err.empty()) j->err = "engine shut down";
+      j->status = NPOW_ERR_NOT_INITIALISED;
+      j->decided = true;
+      j->finished = true;
+    }
+  }
+  g_pool.waiting.clear();
+  g_pool.active.clear();
+  g_pool.cv_done.notify_all();
+}
+
+// -- jobs -------------------------------------------------------------------------------------------
+int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
+                uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket) {
+  auto devs = select_devices(device_mask);
+  if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable device in device_mask");
+  auto j = std::make_shared<Job>();
+  j->pre = host_precompute(root);
+  npow_asm_uniforms(j->pre.m, j->u);
+  j->threshold = threshold;
+  j->start = start;
+  j->max_per_dev = max_nonces_per_device;
+  j->cancel = cancel;
+  const uint64_t G = devs.size();
+  j->spacing = G > 1 ? (~0ull / G) + 1 : 0;  // 2^64 / G (exact for powers of two)
+  for (Device* d : devs) j->devs.push_back(d->id);
+  j->issued.assign(G, 0);
+  j->on_dev.assign(G, 0);
+  j->dev_done.assign(G, 0);
+  j->invalid_streak.assign(G, 0);
+  j->pending_devs = (int)G;
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  if (!g_pool.running) return fail(NPOW_ERR_NOT_INITIALISED, "engine is shut down");
+  j->ticket = g_pool.next_ticket++;
+  g_pool.tickets[j->ticket] = j;
+  g_pool.waiting.push_back(j);
+  admit_locked();
+  *ticket = j->ticket;
+  return NPOW_OK;
+}
+
+int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done) {
+  std::unique_lock<std::mutex> lk(g_pool.mu);
+  auto it = g_pool.tickets.find(ticket);
+  if (it == g_pool.tickets.end()) return fail(NPOW_ERR_BAD_ARGUMENT, "unknown ticket");
+  JobP j = it->second;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us < 0 ? 0 : timeout_us);
+  while (!j->finished) {
+    // a queued job's cancel word is polled here (active ones by the device workers)
+    if (!j->admitted && j->cancel_seen()) {
+      j->cancel_req = true;
+      decide_locked(*j, NPOW_CANCELLED);
+      finish_locked(j);
+      break;
+    }
+    auto wake = std::chrono::steady_clock::now() + std::chrono::microseconds(500);
+    if (timeout_us >= 0) {
+      if (std::chrono::steady_clock::now() >= deadline) return NPOW_PENDING;
+      wake = std::min(wake, deadline);
+    }
+    g_pool.cv_done.wait_until(lk, wake);
+  }
+  if (nonces_done) *nonces_done = j->done;
+  const int st = j->status;
+  g_pool.tickets.erase(ticket);
+  if (st == NPOW_OK) {
+    if (nonce) *nonce = j->nonce;
+    if (value) *value = j->value;
+    return NPOW_OK;
+  }
+  if (st < 0) return fail(st, j->err.empty() ? std::string("work generation failed") : j->err);
+  return st;
+}
+
+int pool_cancel(uint64_t ticket) {
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  auto it = g_pool.tickets.find(ticket);
+  if (it == g_pool.tickets.end()) return fail(NPOW_ERR_BAD_ARGUMENT, "unknown ticket");
+  const JobP& j = it->second;
+  if (j->finished) return NPOW_OK;
+  j->cancel_req = true;
+  if (!j->admitted) {
+    decide_locked(*j, NPOW_CANCELLED);
+    finish_locked(j);
+  }
+  return NPOW_OK;
+}
+
+int pool_set_max_active(uint32_t n) {
+  if (n == 0 || n > (uint32_t)kMaxSlots)
+    return fail(NPOW_ERR_BAD_ARGUMENT, "max_active must be in [1, " + std::to_string(kMaxSlots) + "]");
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  g_pool.max_active = n;
+  admit_locked();
+  return NPOW_OK;
+}
+
+void pool_counts(uint32_t* queued, uint32_t* active) {
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  if (queued) *queued = (uint32_t)g_pool.waiting.size();
+  if (active) *active = (uint32_t)g_pool.active.size();
+}
+
+}  // namespace npow

@@ -9,6 +9,7 @@ client/README.md:31):
   -c/--cpu-threads N            rejected: this engine runs on MI355X GPUs only
   --gpu-local-work-size N       accepted and ignored (workgroups are 256 lanes on gfx950)
   --shuffle                     pick a random queued request instead of the oldest
+  --max-active N                requests searched at once by the GPU work pool (default 4)
 
 Without --gpu every visible GPU is used.
 """
@@ -34,6 +35,9 @@ def parse_args(argv=None) -> argparse.Namespace:
                     default=None, metavar="N", help="Accepted for compatibility; gfx950 workgroups are fixed.")
     ap.add_argument("--shuffle", action="store_true",
                     help="Pick a random request from the queue instead of the oldest.")
+    ap.add_argument("--max-active", type=int, default=4, metavar="N",
+                    help="Requests searched at once by the GPU work pool (1 = strictly one at a time, "
+                         "like the reference; at most 64).")
     ap.add_argument("--base-difficulty", default=W.fmt_u64(W.DEFAULT_BASE),
                     help="Threshold multipliers are quoted against (default fffffff800000000).")
     ap.add_argument("-v", "--verbose", action="store_true")
@@ -67,7 +71,11 @@ def main(argv=None) -> int:
             print(f"GPU {device} not found ({eng.n_devices} visible)", file=sys.stderr)
             return 2
         mask |= 1 << device
-    srv = HttpWorkServer(WorkServer(eng, base_threshold=base, shuffle=args.shuffle, device_mask=mask), host, port_i)
+    if not 1 <= args.max_active <= 64:
+        print("--max-active must be in [1, 64]", file=sys.stderr)
+        return 2
+    srv = HttpWorkServer(WorkServer(eng, base_threshold=base, shuffle=args.shuffle, device_mask=mask,
+                                    max_active=args.max_active), host, port_i)
     logging.info("Configured for the live network with threshold %016x", base)
     logging.info("Ready to receive requests on %s (%d GPU(s), %s)", srv.address,
                  bin(mask).count("1") if mask else eng.n_devices, eng.version())

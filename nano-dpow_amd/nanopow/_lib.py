@@ -21,6 +21,7 @@ LIB_PATH = os.environ.get("NANOPOW_LIB", os.path.join(_HERE, "libnanopow.so"))
 NPOW_OK = 0
 NPOW_CANCELLED = 1
 NPOW_EXHAUSTED = 2
+NPOW_PENDING = 3
 NPOW_ERR_NOT_INITIALISED = -1
 NPOW_ERR_NO_DEVICE = -2
 NPOW_ERR_BAD_ARGUMENT = -3
@@ -35,6 +36,7 @@ EXPORTED_SYMBOLS = (
     "npow_init", "npow_shutdown", "npow_last_error", "npow_work_value", "npow_search",
     "npow_search_batch", "npow_sweep", "npow_values", "npow_values_pairs", "npow_set_tuning",
     "npow_device_stats_get", "npow_device_stats_reset", "npow_version",
+    "npow_submit", "npow_wait", "npow_cancel", "npow_pool_config", "npow_pool_status",
 )
 
 
@@ -109,6 +111,16 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.npow_device_stats_get.restype = ctypes.c_int
         lib.npow_device_stats_reset.argtypes = [ctypes.c_int]
         lib.npow_device_stats_reset.restype = ctypes.c_int
+        lib.npow_submit.argtypes = [u8p, u64, u64, u64, u64, p, pu64]
+        lib.npow_submit.restype = ctypes.c_int
+        lib.npow_wait.argtypes = [u64, ctypes.c_int64, pu64, pu64, pu64]
+        lib.npow_wait.restype = ctypes.c_int
+        lib.npow_cancel.argtypes = [u64]
+        lib.npow_cancel.restype = ctypes.c_int
+        lib.npow_pool_config.argtypes = [u32]
+        lib.npow_pool_config.restype = ctypes.c_int
+        lib.npow_pool_status.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
+        lib.npow_pool_status.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -147,6 +159,37 @@ class CancelToken:
         return ctypes.addressof(self._word)
 
 
+class Ticket:
+    """A submitted search (npow_submit); wait() returns its SearchResult once."""
+
+    def __init__(self, engine: "Engine", ticket: int, cancel: Optional[CancelToken]) -> None:
+        self.engine = engine
+        self.ticket = ticket
+        self.cancel_token = cancel  # keeps the cancel word alive while the engine may read it
+        self.result: Optional[SearchResult] = None
+
+    def wait(self, timeout: Optional[float] = None) -> Optional[SearchResult]:
+        """Block until the search ends (timeout None) or up to `timeout` seconds; None if
+        it is still running then."""
+        if self.result is not None:
+            return self.result
+        lib = self.engine.lib
+        nonce, value, done = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        us = -1 if timeout is None else max(0, int(timeout * 1e6))
+        rc = lib.npow_wait(self.ticket, us, ctypes.byref(nonce), ctypes.byref(value), ctypes.byref(done))
+        if rc == NPOW_PENDING:
+            return None
+        self.cancel_token = None
+        _check(rc, lib, ok=(NPOW_OK, NPOW_CANCELLED, NPOW_EXHAUSTED))
+        self.result = (SearchResult(rc, nonce.value, value.value, done.value) if rc == NPOW_OK
+                       else SearchResult(rc, None, None, done.value))
+        return self.result
+
+    def cancel(self) -> None:
+        if self.result is None:
+            _check(self.engine.lib.npow_cancel(self.ticket), self.engine.lib)
+
+
 class Engine:
     """Thin object wrapper over the C ABI (one per process is enough)."""
 
@@ -173,6 +216,24 @@ class Engine:
         if rc == NPOW_OK:
             return SearchResult(rc, nonce.value, value.value, done.value)
         return SearchResult(rc, None, None, done.value)
+
+    # -- work pool: asynchronous searches ---------------------------------------------------
+    def submit(self, root: bytes, threshold: int, start: int = 0, device_mask: int = 0,
+               max_nonces_per_device: int = 0, cancel: Optional[CancelToken] = None) -> "Ticket":
+        """Queue a first-win search and return at once (npow_submit).  Keep `cancel` alive
+        until the ticket's result has been collected (the Ticket holds a reference)."""
+        t = ctypes.c_uint64(0)
+        _check(self.lib.npow_submit(_root(root), threshold & M64, start & M64, device_mask, max_nonces_per_device,
+                                    cancel.address if cancel else None, ctypes.byref(t)), self.lib)
+        return Ticket(self, t.value, cancel)
+
+    def pool_config(self, max_active: int) -> None:
+        _check(self.lib.npow_pool_config(max_active), self.lib)
+
+    def pool_status(self) -> Tuple[int, int]:
+        q, a = ctypes.c_uint32(0), ctypes.c_uint32(0)
+        _check(self.lib.npow_pool_status(ctypes.byref(q), ctypes.byref(a)), self.lib)
+        return q.value, a.value
 
     def search_batch(self, roots: Sequence[bytes], thresholds: Sequence[int], device_mask: int = 0,
                      max_nonces_per_root: int = 0,

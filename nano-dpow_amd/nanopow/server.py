@@ -20,10 +20,14 @@ Also served: ``work_validate`` (valid / valid_all / valid_receive / difficulty /
 multiplier, @1680400..1680528), ``status`` (generating / queue_size,
 @1679680) and ``benchmark`` (count -> duration / average / hint, @1679992..1680344).
 
-Requests queue FIFO (``--shuffle``: random pick, nano-work-server.exe @1681064);
-each root is searched by every selected GPU at once (libnanopow first-win
-search).  Every reply a search produces was re-validated on the CPU inside
-libnanopow before it reaches this layer.
+Requests queue FIFO (``--shuffle``: random pick, nano-work-server.exe @1681064).
+The reference serves one request at a time; here up to ``max_active`` queued
+requests are handed to libnanopow's work pool at once (npow_submit), where
+every selected GPU searches all of them in the same kernel launches, so a
+burst of requests from many clients keeps the GPUs busy across request
+boundaries.  ``max_active=1`` is the reference's strictly serial service.
+Every reply a search produces was re-validated on the CPU inside libnanopow
+before it reaches this layer.
 """
 from __future__ import annotations
 
@@ -42,17 +46,21 @@ from ._lib import NPOW_CANCELLED, NPOW_OK, CancelToken, NanoPowError, SearchResu
 log = logging.getLogger("nanopow.server")
 
 
+class SearchTicket(Protocol):
+    def wait(self, timeout: Optional[float] = None) -> Optional[SearchResult]: ...
+
+
 class SearchEngine(Protocol):
     """What the server needs from an engine (libnanopow's :class:`nanopow.Engine`)."""
 
-    def search(self, root: bytes, threshold: int, start: int = 0, device_mask: int = 0,
-               max_nonces_per_device: int = 0, cancel: Optional[CancelToken] = None) -> SearchResult: ...
+    def submit(self, root: bytes, threshold: int, start: int = 0, device_mask: int = 0,
+               max_nonces_per_device: int = 0, cancel: Optional[CancelToken] = None) -> SearchTicket: ...
 
     def work_value(self, root: bytes, nonce: int) -> int: ...
 
 
 class Job:
-    __slots__ = ("root", "threshold", "cancel", "done", "reply", "active", "t_queued", "waiters")
+    __slots__ = ("root", "threshold", "cancel", "done", "reply", "active", "t_queued", "waiters", "t_started")
 
     def __init__(self, root: bytes, threshold: int) -> None:
         self.root = root
@@ -62,6 +70,7 @@ class Job:
         self.reply: Dict[str, Any] = {}
         self.active = False
         self.t_queued = time.perf_counter()
+        self.t_started = 0.0
         self.waiters = 1
 
     def resolve(self, reply: Dict[str, Any]) -> None:
@@ -71,20 +80,23 @@ class Job:
 
 
 class WorkServer:
-    """Request dispatcher + single search worker (all selected GPUs per root)."""
+    """Request dispatcher: a FIFO (or shuffled) queue in front of the engine's work pool."""
 
     def __init__(self, engine: SearchEngine, base_threshold: int = W.DEFAULT_BASE, shuffle: bool = False,
-                 device_mask: int = 0, rng: Optional[random.Random] = None) -> None:
+                 device_mask: int = 0, rng: Optional[random.Random] = None, max_active: int = 4) -> None:
+        if max_active < 1:
+            raise ValueError("max_active must be >= 1")
         self.engine = engine
         self.base = base_threshold
         self.shuffle = shuffle
         self.device_mask = device_mask
+        self.max_active = max_active
         self.rng = rng or random.Random(int.from_bytes(os.urandom(8), "little"))
         self._lock = threading.Condition()
         self._queue: List[Job] = []
-        self._active: Optional[Job] = None
+        self._inflight: List[Job] = []
         self._running = False
-        self._worker: Optional[threading.Thread] = None
+        self._dispatcher: Optional[threading.Thread] = None
 
     # -- lifecycle ---------------------------------------------------------------------
     def start(self) -> "WorkServer":
@@ -92,8 +104,8 @@ class WorkServer:
             if self._running:
                 return self
             self._running = True
-        self._worker = threading.Thread(target=self._work_loop, name="nanopow-worker", daemon=True)
-        self._worker.start()
+        self._dispatcher = threading.Thread(target=self._dispatch_loop, name="nanopow-dispatch", daemon=True)
+        self._dispatcher.start()
         return self
 
     def stop(self) -> None:
@@ -101,13 +113,17 @@ class WorkServer:
             self._running = False
             pending = list(self._queue)
             self._queue.clear()
-            if self._active is not None:
-                self._active.cancel.set()
+            for j in self._inflight:
+                j.cancel.set()
             self._lock.notify_all()
         for j in pending:
             j.resolve({"error": "Cancelled"})
-        if self._worker is not None:
-            self._worker.join(timeout=10)
+        if self._dispatcher is not None:
+            self._dispatcher.join(timeout=10)
+        deadline = time.time() + 10
+        with self._lock:
+            while self._inflight and time.time() < deadline:
+                self._lock.wait(0.1)
 
     # -- dispatch ----------------------------------------------------------------------
     def handle(self, req: Any) -> Dict[str, Any]:
@@ -144,8 +160,9 @@ class WorkServer:
             for j in self._queue:
                 (cancelled if j.root == root else keep).append(j)
             self._queue[:] = keep
-            if self._active is not None and self._active.root == root:
-                self._active.cancel.set()
+            for j in self._inflight:
+                if j.root == root:
+                    j.cancel.set()
         for j in cancelled:
             j.resolve({"error": "Cancelled"})
         log.info("Cancel %s", root.hex().upper())
@@ -167,7 +184,7 @@ class WorkServer:
 
     def status(self) -> Dict[str, Any]:
         with self._lock:
-            return {"generating": "1" if self._active is not None else "0", "queue_size": str(len(self._queue))}
+            return {"generating": "1" if self._inflight else "0", "queue_size": str(len(self._queue))}
 
     def benchmark(self, req: Dict[str, Any]) -> Dict[str, Any]:
         count = W.parse_count(req)
@@ -194,7 +211,7 @@ class WorkServer:
                 j.resolve({"error": "Work generation failed (see logs for details)"})
                 return j
             # the same root at the same threshold queued or running: share its result
-            for j in ([self._active] if self._active else []) + self._queue:
+            for j in self._inflight + self._queue:
                 if j.root == root and j.threshold == threshold and not j.cancel.is_set:
                     j.waiters += 1
                     return j
@@ -205,44 +222,57 @@ class WorkServer:
 
     def _next_job(self) -> Optional[Job]:
         with self._lock:
-            while self._running and not self._queue:
+            while self._running and (not self._queue or len(self._inflight) >= self.max_active):
                 self._lock.wait()
             if not self._running:
                 return None
             idx = self.rng.randrange(len(self._queue)) if self.shuffle else 0
             job = self._queue.pop(idx)
             job.active = True
-            self._active = job
+            self._inflight.append(job)
             return job
 
-    def _work_loop(self) -> None:
+    def _dispatch_loop(self) -> None:
         while True:
             job = self._next_job()
             if job is None:
                 return
-            t0 = time.perf_counter()
+            job.t_started = time.perf_counter()
             try:
-                start = self.rng.getrandbits(64)
-                res = self.engine.search(job.root, job.threshold, start=start, device_mask=self.device_mask,
-                                         cancel=job.cancel)
-                if res.status == NPOW_OK:
-                    reply = {"work": W.fmt_u64(res.nonce), "difficulty": W.fmt_u64(res.value),
-                             "multiplier": W.fmt_multiplier(W.to_multiplier(res.value, self.base))}
-                    log.info("Generated for %s in %.0fms for difficulty %016x", job.root.hex().upper(),
-                             (time.perf_counter() - t0) * 1000.0, job.threshold)
-                elif res.status == NPOW_CANCELLED:
-                    reply = {"error": "Cancelled"}
-                else:
-                    reply = {"error": "Work generation failed (see logs for details)"}
-            except NanoPowError as e:
-                log.error("Error computing work: %s", e)
-                reply = {"error": "Work generation failed (see logs for details)"}
+                ticket = self.engine.submit(job.root, job.threshold, start=self.rng.getrandbits(64),
+                                            device_mask=self.device_mask, cancel=job.cancel)
             except Exception as e:  # never leave a client waiting
-                log.exception("work loop failure: %s", e)
+                log.error("Error computing work: %s", e)
+                self._complete(job, {"error": "Work generation failed (see logs for details)"})
+                continue
+            threading.Thread(target=self._await, args=(job, ticket), name="nanopow-await", daemon=True).start()
+
+    def _await(self, job: Job, ticket: SearchTicket) -> None:
+        try:
+            res = ticket.wait()
+            if res is not None and res.status == NPOW_OK:
+                reply = {"work": W.fmt_u64(res.nonce), "difficulty": W.fmt_u64(res.value),
+                         "multiplier": W.fmt_multiplier(W.to_multiplier(res.value, self.base))}
+                log.info("Generated for %s in %.0fms for difficulty %016x", job.root.hex().upper(),
+                         (time.perf_counter() - job.t_started) * 1000.0, job.threshold)
+            elif res is not None and res.status == NPOW_CANCELLED:
+                reply = {"error": "Cancelled"}
+            else:
                 reply = {"error": "Work generation failed (see logs for details)"}
-            with self._lock:
-                self._active = None
-            job.resolve(reply)
+        except NanoPowError as e:
+            log.error("Error computing work: %s", e)
+            reply = {"error": "Work generation failed (see logs for details)"}
+        except Exception as e:  # never leave a client waiting
+            log.exception("work loop failure: %s", e)
+            reply = {"error": "Work generation failed (see logs for details)"}
+        self._complete(job, reply)
+
+    def _complete(self, job: Job, reply: Dict[str, Any]) -> None:
+        job.resolve(reply)
+        with self._lock:
+            if job in self._inflight:
+                self._inflight.remove(job)
+            self._lock.notify_all()
 
 
 # ---------------------------------------------------------------------------------------

@@ -11,6 +11,20 @@ import oracle
 from nanopow._lib import NPOW_CANCELLED, NPOW_EXHAUSTED, NPOW_OK, SearchResult
 
 
+class _Ticket:
+    def __init__(self, fn):
+        self._ev = threading.Event()
+        self._res = None
+
+        def run():
+            self._res = fn()
+            self._ev.set()
+        threading.Thread(target=run, daemon=True).start()
+
+    def wait(self, timeout=None):
+        return self._res if self._ev.wait(timeout) else None
+
+
 class OracleEngine:
     n_devices = 1
 
@@ -41,3 +55,6 @@ class OracleEngine:
             n += cnt
             if self.delay:
                 time.sleep(self.delay)
+
+    def submit(self, root, threshold, start=0, device_mask=0, max_nonces_per_device=0, cancel=None):
+        return _Ticket(lambda: self.search(root, threshold, start, device_mask, max_nonces_per_device, cancel))

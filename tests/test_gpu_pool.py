@@ -1,0 +1,136 @@
+"""GPU work pool (npow_submit / npow_wait / npow_cancel; npow_pool_kernel): many roots per launch.
+
+Bit-exact against the oracle throughout: every winner re-validates under hashlib at its own
+threshold, every bounded range without a hit is reported EXHAUSTED with exactly its nonce
+count hashed, every bounded range with hits returns one of the fixture's hits, and the
+nonces the jobs report add up to the device's own counter.  Run on an MI355X: ``pytest -m gpu``.
+"""
+import random
+import time
+
+import pytest
+
+import oracle
+from conftest import load_golden
+from nanopow import _lib
+
+pytestmark = pytest.mark.gpu
+M64 = (1 << 64) - 1
+SEND, RECEIVE, LOW = 0xfffffff800000000, 0xfffffe0000000000, 0xfffff00000000000
+
+
+def _roots(seed, n):
+    rng = random.Random(seed)
+    return [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(n)]
+
+
+def test_many_roots_in_flight_all_revalidate(gpu_engine):
+    """200 roots at three thresholds submitted at once: up to 64 share each launch."""
+    roots = _roots(11, 200)
+    thr = [LOW, RECEIVE, 0xffffc00000000000]
+    tickets = [gpu_engine.submit(r, thr[i % 3], start=i << 48) for i, r in enumerate(roots)]
+    for i, (r, t) in enumerate(zip(roots, tickets)):
+        res = t.wait(60)
+        assert res is not None and res.status == _lib.NPOW_OK, i
+        assert oracle.work_value_hashlib(r, res.nonce) == res.value >= thr[i % 3]
+        assert res.nonces_done > 0
+
+
+def test_nonce_accounting_matches_device_counter(gpu_engine):
+    """Jobs that win, are cancelled, and keep running side by side (waves migrate between
+    them): the nonces each job reports sum to what the device counted."""
+    gpu_engine.reset_stats(0)
+    roots = _roots(12, 40)
+    toks = [_lib.CancelToken() for _ in range(8)]
+    never = [gpu_engine.submit(r, M64, start=7 << 50, device_mask=1, cancel=c) for r, c in zip(roots[:8], toks)]
+    quick = [gpu_engine.submit(r, LOW, device_mask=1) for r in roots[8:]]
+    done = 0
+    for r, t in zip(roots[8:], quick):
+        res = t.wait(60)
+        assert res.status == _lib.NPOW_OK and oracle.work_value(r, res.nonce) == res.value >= LOW
+        done += res.nonces_done
+    time.sleep(0.05)
+    for c in toks:
+        c.set()
+    for t in never:
+        res = t.wait(30)
+        assert res.status == _lib.NPOW_CANCELLED and res.nonces_done > 0
+        done += res.nonces_done
+    st = gpu_engine.stats(0)
+    assert st.nonces == done
+
+
+def test_bounded_ranges_exact_beside_unbounded_jobs(gpu_engine):
+    """Bounded ranges (max_nonces) are covered exactly once even while unbounded jobs in the
+    same launches hand waves around: gaps between consecutive fixture hits are EXHAUSTED
+    after exactly gap nonces; ranges that hold hits return one of them."""
+    c = load_golden("sweeps_small.json")["cases"][1]  # RECEIVE hits of root 0 in [0, 2^28)
+    root, thr = bytes.fromhex(c["root"]), int(c["threshold"], 16)
+    hits = [int(h, 16) for h in c["hits"]]
+    tok = _lib.CancelToken()
+    busy = [gpu_engine.submit(r, M64, device_mask=1, cancel=tok) for r in _roots(13, 4)]
+    gaps = [(hits[i] + 1, hits[i + 1] - hits[i] - 1) for i in range(min(12, len(hits) - 1))]
+    gap_t = [gpu_engine.submit(root, thr, start=s, device_mask=1, max_nonces_per_device=n) for s, n in gaps]
+    span_t = [gpu_engine.submit(root, thr, start=hits[i] - 5, device_mask=1, max_nonces_per_device=1000)
+              for i in range(4)]
+    for (s, n), t in zip(gaps, gap_t):
+        res = t.wait(60)
+        assert res.status == _lib.NPOW_EXHAUSTED and res.nonce is None
+        assert res.nonces_done == n
+    for i, t in enumerate(span_t):
+        res = t.wait(60)
+        assert res.status == _lib.NPOW_OK and res.nonce == hits[i]  # the only hit in its range
+    tok.set()
+    for t in busy:
+        assert t.wait(30).status == _lib.NPOW_CANCELLED
+
+
+def test_wait_timeout_and_ticket_cancel(gpu_engine):
+    t = gpu_engine.submit(bytes(32), M64, device_mask=1)
+    assert t.wait(0.01) is None
+    q, a = gpu_engine.pool_status()
+    assert a >= 1
+    t.cancel()
+    res = t.wait(10)
+    assert res.status == _lib.NPOW_CANCELLED and res.nonces_done > 0
+
+
+def test_max_active_queues_the_rest(gpu_engine):
+    gpu_engine.pool_config(2)
+    try:
+        toks = [_lib.CancelToken() for _ in range(5)]
+        ts = [gpu_engine.submit(r, M64, device_mask=1, cancel=c) for r, c in zip(_roots(14, 5), toks)]
+        time.sleep(0.05)
+        assert gpu_engine.pool_status() == (3, 2)
+        toks[4].set()  # a queued job cancelled before it ever ran
+        res = ts[4].wait(10)
+        assert res.status == _lib.NPOW_CANCELLED and res.nonces_done == 0
+        for c in toks[:4]:
+            c.set()
+        for t in ts[:4]:
+            assert t.wait(30).status == _lib.NPOW_CANCELLED
+    finally:
+        gpu_engine.pool_config(64)
+    assert gpu_engine.pool_status() == (0, 0)
+
+
+def test_sweep_waits_for_the_device_and_both_finish(gpu_engine):
+    root = bytes(range(3, 35))
+    tickets = [gpu_engine.submit(r, RECEIVE, device_mask=1) for r in _roots(15, 8)]
+    hits = gpu_engine.sweep(root, 0xffff000000000000, 0, 1 << 22, device_mask=1)
+    assert hits == oracle.sweep(root, 0xffff000000000000, 0, 1 << 22)
+    for t in tickets:
+        assert t.wait(60).status == _lib.NPOW_OK
+
+
+def test_batch_of_64_with_cancels(gpu_engine):
+    roots = _roots(16, 64)
+    thr = [RECEIVE] * 48 + [M64] * 16
+    toks = [None] * 48 + [_lib.CancelToken() for _ in range(16)]
+    for c in toks[48:]:
+        c.set()
+    res, done = gpu_engine.search_batch(roots, thr, cancels=toks)
+    for r, x in zip(roots[:48], res[:48]):
+        assert x.status == _lib.NPOW_OK and oracle.work_value(r, x.nonce) == x.value >= RECEIVE
+    assert all(x.status == _lib.NPOW_CANCELLED for x in res[48:])
+    assert done > 0

@@ -33,7 +33,7 @@ def post(addr, obj, timeout=30):
 @pytest.fixture()
 def server():
     eng = OracleEngine(chunk=1 << 12, delay=0.001)
-    srv = HttpWorkServer(WorkServer(eng), "127.0.0.1", 0).start()
+    srv = HttpWorkServer(WorkServer(eng, max_active=1), "127.0.0.1", 0).start()  # the reference: serial
     yield srv, eng
     srv.stop()
 
@@ -199,3 +199,39 @@ def test_shuffle_picks_all_requests():
         assert len(out) == 6 and all("work" in r for r in out)
     finally:
         ws.stop()
+
+
+def test_concurrent_requests_share_the_pool():
+    """max_active > 1: several requests are in the engine at once (npow_submit), the rest
+    queue FIFO; a queued request starts when one in flight ends; status counts both."""
+    eng = OracleEngine(chunk=1 << 12, delay=0.001)
+    srv = HttpWorkServer(WorkServer(eng, max_active=3), "127.0.0.1", 0).start()
+    try:
+        holds = [{"action": "work_generate", "hash": f"{0x40 + i:02x}" * 32, "difficulty": "ffffffffffffffff"}
+                 for i in range(3)]
+        out = {}
+        ths = [threading.Thread(target=lambda i=i: out.setdefault(i, post(srv.address, holds[i]))) for i in range(3)]
+        for t in ths:
+            t.start()
+        deadline = time.time() + 10
+        while time.time() < deadline and len(eng.calls) < 3:
+            time.sleep(0.02)
+        assert len(eng.calls) == 3
+        root = bytes(range(32))
+        req = {"action": "work_generate", "hash": root.hex(), "difficulty": "ffff000000000000"}
+        tq = threading.Thread(target=lambda: out.setdefault("q", post(srv.address, req)))
+        tq.start()
+        time.sleep(0.3)
+        assert post(srv.address, {"action": "status"}) == {"generating": "1", "queue_size": "1"}
+        assert "q" not in out
+        post(srv.address, {"action": "work_cancel", "hash": holds[0]["hash"]})
+        tq.join(20)
+        assert oracle.work_value(root, int(out["q"]["work"], 16)) >= 0xffff000000000000
+        for h in holds[1:]:
+            post(srv.address, {"action": "work_cancel", "hash": h["hash"]})
+        for t in ths:
+            t.join(10)
+        assert all(out[i] == {"error": "Cancelled"} for i in range(3))
+        assert post(srv.address, {"action": "status"}) == {"generating": "0", "queue_size": "0"}
+    finally:
+        srv.stop()
