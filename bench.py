@@ -19,7 +19,7 @@ its own roots on its own GPU (disjoint work, no data-path collective); gloo on
 the CPU carries only the barrier and the max/sum of the timings.
 Scaling is therefore "weak" (fixed searches per GPU).
 
-roofline: the dominant kernel (npow_task_kernel<kSearch>) is int32-VALU bound.
+roofline: the dominant kernel (npow_pool_kernel<false>) is int32-VALU bound.
 achieved = nonces hashed in kernel x 2232 int32 ops/nonce /
 kernel time, the kernel time measured by HIP events recorded on the stream the
 kernel runs on (libnanopow stats); peak = 256 CUs x 128 int32 lanes/clk
@@ -27,6 +27,16 @@ kernel runs on (libnanopow stats); peak = 256 CUs x 128 int32 lanes/clk
 cpu_baseline (rank 0, N=1 only): the oracle's C restatement of the same work
 value (oracle/blake2b_oracle.c, "port"), exhaustive scan of a bounded sample of
 R_0's nonce space on the host cores; hashlib single-core rate alongside.
+
+Other BASELINE.json configurations (``--workload``; not the driver's default line):
+  allgpus   one process, every visible GPU on ONE root at a time (first win across
+            GPUs, disjoint strides): p50/p99 time-to-work at N GPUs (config 2 at N>1);
+  sweep     config 3: every hit of [0, 2^36) for the fixture root, ranks split the range,
+            hit set compared with tests/golden/sweep_2p36.json (exact);
+  burst     config 4: --roots requests at fffffff8 submitted at once to the work pool
+            (npow_submit), 25 % cancelled at uniform times in [0, 0.5 x the expected
+            burst time); every reply re-validated on the CPU (libnanopow npow_work_value);
+  sustained config 5: --duration seconds of back-to-back fresh roots, --depth in flight.
 """
 from __future__ import annotations
 
@@ -160,7 +170,7 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
         "gnps_per_gpu": round(gnps / world, 4),
         "roofline": {
             "bound": "valu",
-            "kernel": "npow_task_kernel<Mode::kSearch>",
+            "kernel": "npow_pool_kernel<false>",
             "achieved": round(achieved, 3),
             "peak": round(PEAK_TOPS, 3),
             "unit": "Tops/s (int32 VALU)",
@@ -175,6 +185,198 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
     }
 
 
+def _reduce(dist, nonces, wall, ttw, extra_sum=()):
+    """Sum nonces (and extra_sum values) over ranks, max wall, gather ttw."""
+    if dist is None:
+        return nonces, wall, ttw, list(extra_sum)
+    import torch
+    v = torch.tensor([float(nonces)] + [float(x) for x in extra_sum], dtype=torch.float64)
+    dist.all_reduce(v, op=dist.ReduceOp.SUM)
+    w_t = torch.tensor([wall], dtype=torch.float64)
+    dist.all_reduce(w_t, op=dist.ReduceOp.MAX)
+    gathered = [None] * dist.get_world_size()
+    dist.all_gather_object(gathered, ttw)
+    return int(v[0]), float(w_t[0]), [x for g in gathered for x in g], [float(x) for x in v[1:]]
+
+
+def workload_allgpus(eng, args, rank, world, dist):
+    """One process, every visible GPU on one root at a time (npow_search, device_mask 0)."""
+    if world > 1:
+        raise SystemExit("--workload allgpus runs in ONE process (it drives every GPU itself)")
+    n_dev = eng.n_devices
+
+    def search(i):
+        t = time.perf_counter()
+        r = eng.search(bench_root(i), SEND, start=bench_start(i), device_mask=0)
+        if r.status != 0:
+            raise RuntimeError(f"search {i} returned status {r.status}")
+        return time.perf_counter() - t, r.nonces_done
+
+    def stats():
+        ks = [eng.stats(d) for d in range(n_dev)]
+        return sum(k.kernel_ms for k in ks) / n_dev, sum(k.nonces for k in ks), sum(k.launches for k in ks)
+
+    def reset():
+        for d in range(n_dev):
+            eng.reset_stats(d)
+
+    nonces, wall, ttw, kern_ms, kern_nonces, launches = run_timed(search, stats, reset, args.steps, args.warmup,
+                                                                  rank, 1, None)
+    line = result_line(1, args.steps, args.warmup, nonces, wall, ttw, kern_ms * n_dev, kern_nonces, launches)
+    line["n_gpus"] = n_dev
+    line["gnps_per_gpu"] = round(line["value"] / n_dev, 4)
+    line["scaling"] = "strong"
+    line["config"]["workload"] = (f"BASELINE configs[1] at N={n_dev}: one root at a time searched by every GPU "
+                                  "of the process on disjoint strides, first win across GPUs")
+    line["config"]["parallelism"] = f"in-process x{n_dev} (first-win flag only, no collective)"
+    return line
+
+
+def workload_sweep(eng, args, rank, world, dist):
+    """BASELINE config 3: every valid nonce of [0, 2^bits) for the fixture root, exact."""
+    import json as _json
+    with open(os.path.join(HERE, "tests", "golden", "sweep_2p36.json")) as f:
+        fx = _json.load(f)
+    root, thr = bytes.fromhex(fx["root"]), int(fx["threshold"], 16)
+    count = 1 << args.sweep_bits
+    per = count // world
+    lo = rank * per
+    n_here = per if rank < world - 1 else count - lo
+    eng.reset_stats(0)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    hits = eng.sweep(root, thr, lo, n_here, device_mask=1, cap=1 << 16)
+    wall = time.perf_counter() - t0
+    st = eng.stats(0)
+    nonces, wall, _, (kms, kn, nl) = _reduce(dist, n_here, wall, [], (st.kernel_ms, st.nonces, st.launches))
+    if dist is not None:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, hits)
+        hits = sorted(h for g in gathered for h in g)
+    want = [int(h, 16) for h in fx["hits"] if int(h, 16) < count]
+    line = result_line(world, 1, 0, nonces, wall, [wall], kms, kn, nl)
+    line["roofline"]["kernel"] = "npow_task_kernel<Mode::kSweep>"
+    line["config"] = {"workload": f"BASELINE configs[2]: exhaustive sweep of [0, 2^{args.sweep_bits}) for the "
+                                  "fixture root at fffffff800000000, ranks split the range",
+                      "threshold": fx["threshold"], "count": count,
+                      "parallelism": f"dp{world} (contiguous sub-ranges, no collective on the data path)"}
+    line["hits"] = len(hits)
+    line["hits_exact_vs_fixture"] = hits == want
+    if hits != want:
+        raise RuntimeError(f"sweep hit set differs from the fixture ({len(hits)} vs {len(want)})")
+    return line
+
+
+def workload_burst(eng, args, rank, world, dist):
+    """BASELINE config 4: a burst of --roots concurrent requests with 25 % mid-search cancels."""
+    import queue
+    import random
+    import threading
+    from nanopow import _lib
+    n = args.roots
+    rng = random.Random(4242 + rank)
+    idx = [7_000_000 + rank * 1_000_000 + i for i in range(n)]
+    roots = [bench_root(i) for i in idx]
+    toks = [_lib.CancelToken() for _ in range(n)]
+    cancel_set = set(rng.sample(range(n), n // 4))
+    est = n * float(1 << 29) / (25e9 * max(1, eng.n_devices if world == 1 else 1))
+    cancel_at = sorted((rng.uniform(0.0, 0.5 * est), i) for i in cancel_set)
+    eng.reset_stats(0)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    tickets = [eng.submit(roots[i], SEND, start=bench_start(idx[i]), device_mask=0 if world == 1 else 1,
+                          cancel=toks[i]) for i in range(n)]
+
+    def canceller():
+        for t_c, i in cancel_at:
+            dt = t0 + t_c - time.perf_counter()
+            if dt > 0:
+                time.sleep(dt)
+            toks[i].set()
+    th_c = threading.Thread(target=canceller, daemon=True)
+    th_c.start()
+    q: "queue.Queue[int]" = queue.Queue()
+    for i in range(n):
+        q.put(i)
+    done_at, results = [0.0] * n, [None] * n
+
+    def waiter():
+        while True:
+            try:
+                i = q.get_nowait()
+            except queue.Empty:
+                return
+            results[i] = tickets[i].wait()
+            done_at[i] = time.perf_counter() - t0
+    ws = [threading.Thread(target=waiter) for _ in range(64)]
+    for w in ws:
+        w.start()
+    for w in ws:
+        w.join()
+    wall = time.perf_counter() - t0
+    th_c.join(0)
+    ok = [i for i in range(n) if results[i].status == 0]
+    bad = [i for i in ok if eng.work_value(roots[i], results[i].nonce) != results[i].value
+           or results[i].value < SEND]
+    unc_fail = [i for i in range(n) if i not in cancel_set and results[i].status != 0]
+    canc_ok = sum(1 for i in cancel_set if results[i].status == 0)
+    nonces = sum(r.nonces_done for r in results)
+    ttw = [done_at[i] for i in ok]
+    st = eng.stats(0)
+    nonces, wall, ttw, (kms, kn, nl, n_bad, n_uf) = _reduce(dist, nonces, wall, ttw,
+                                                            (st.kernel_ms, st.nonces, st.launches, len(bad),
+                                                             len(unc_fail)))
+    line = result_line(world, n, 0, nonces, wall, ttw or [0.0], kms, kn, nl)
+    line["config"] = {"workload": f"BASELINE configs[3]: burst of {n} concurrent requests per GPU at "
+                                  "fffffff800000000 through the work pool, 25 % cancelled mid-search",
+                      "threshold": "fffffff800000000", "roots_per_gpu": n,
+                      "parallelism": f"dp{world} (disjoint roots per GPU)" if world > 1 else
+                                     f"work pool over {eng.n_devices} GPU(s)"}
+    line["burst"] = {"ok": len(ok), "cancelled_requested": len(cancel_set),
+                     "cancel_lost_race": canc_ok, "invalid_replies": int(n_bad),
+                     "uncancelled_failures": int(n_uf)}
+    if n_bad or n_uf:
+        raise RuntimeError(f"burst: {int(n_bad)} invalid replies, {int(n_uf)} uncancelled failures")
+    return line
+
+
+def workload_sustained(eng, args, rank, world, dist):
+    """BASELINE config 5: --duration seconds of fresh roots, --depth requests in flight per GPU."""
+    from collections import deque
+    eng.reset_stats(0)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+    pending = deque()
+    nxt, nonces, ttw = 0, 0, []
+    base = 9_000_000 + rank * 10_000_000
+    while True:
+        now = time.perf_counter()
+        while len(pending) < args.depth and now - t0 < args.duration:
+            i = base + nxt
+            nxt += 1
+            pending.append((eng.submit(bench_root(i), SEND, start=bench_start(i), device_mask=1), now))
+        if not pending:
+            break
+        t, ts = pending.popleft()
+        r = t.wait()
+        if r.status != 0:
+            raise RuntimeError(f"sustained: status {r.status}")
+        nonces += r.nonces_done
+        ttw.append(time.perf_counter() - ts)
+    wall = time.perf_counter() - t0
+    st = eng.stats(0)
+    nonces, wall, ttw, (kms, kn, nl) = _reduce(dist, nonces, wall, ttw, (st.kernel_ms, st.nonces, st.launches))
+    line = result_line(world, len(ttw), 0, nonces, wall, ttw, kms, kn, nl)
+    line["config"] = {"workload": f"BASELINE configs[4]: {args.duration:.0f} s of back-to-back fresh roots at "
+                                  f"fffffff800000000, {args.depth} in flight per GPU",
+                      "threshold": "fffffff800000000", "duration_s": args.duration, "depth": args.depth,
+                      "parallelism": f"dp{world} (per-GPU roots and strides, no collective)"}
+    return line
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -182,6 +384,11 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--iters", type=int, default=0, help="override wave iterations per launch")
+    ap.add_argument("--workload", default="search", choices=["search", "allgpus", "sweep", "burst", "sustained"])
+    ap.add_argument("--sweep-bits", type=int, default=36, help="sweep: range [0, 2^bits)")
+    ap.add_argument("--roots", type=int, default=4096, help="burst: requests per GPU")
+    ap.add_argument("--duration", type=float, default=60.0, help="sustained: seconds")
+    ap.add_argument("--depth", type=int, default=4, help="sustained: requests in flight per GPU")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -196,6 +403,16 @@ def main() -> int:
     if args.iters:
         eng.set_tuning(args.iters, 0, 0)
     dev = 0
+    if args.workload != "search":
+        fn = {"allgpus": workload_allgpus, "sweep": workload_sweep, "burst": workload_burst,
+              "sustained": workload_sustained}[args.workload]
+        line = fn(eng, args, rank, WORLD, dist)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if dist is not None:
+            dist.barrier()
+            dist.destroy_process_group()
+        return 0
 
     def search(i):
         t = time.perf_counter()

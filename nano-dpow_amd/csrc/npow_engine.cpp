@@ -233,10 +233,14 @@ int npow_init(int* n_devices) {
   pool_start();
   static bool exit_hook = false;
   if (!exit_hook) {
-    // Join the pool's worker threads before static destructors and the HIP runtime's own
-    // exit-time teardown (registered earlier by hipGetDeviceCount, so it runs after this).
+    // Join the pool's worker threads before static destructors run (a joinable std::thread
+    // would terminate the process).  No HIP calls here: by now a profiler or the runtime may
+    // have torn its state down; the OS reclaims device memory with the process.
     exit_hook = true;
-    atexit([] { npow_shutdown(); });
+    atexit([] {
+      std::lock_guard<std::mutex> g(g_mu);
+      if (g_init) pool_exit();
+    });
   }
   if (n_devices) *n_devices = (int)g_devs.size();
   return NPOW_OK;

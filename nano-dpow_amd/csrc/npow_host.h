@@ -87,6 +87,7 @@ int pool_device_init(Device& d);     // allocate pool buffers of one device
 void pool_device_free(Device& d);
 void pool_start();                   // start one worker thread per device
 void pool_stop();                    // stop and join the workers (pending jobs end with an error)
+void pool_exit();                    // process exit: join the workers without further HIP calls
 int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
                 uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket);
 int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done);

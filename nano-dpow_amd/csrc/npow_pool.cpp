@@ -81,6 +81,7 @@ struct Pool {
 } g_pool;
 
 std::atomic<uint64_t> g_gen{0};
+std::atomic<bool> g_exiting{false};  // process exit: workers leave at once, no further HIP calls
 
 // -- job state transitions (caller holds g_pool.mu) ------------------------------------------
 void decide_locked(Job& j, int status, uint64_t nonce = 0, uint64_t value = 0) {
@@ -420,6 +421,7 @@ int Worker::step() {
 void Worker::run() {
   if (hipSetDevice(d_.id) != hipSuccess) d_.dead = true;
   for (;;) {
+    if (g_exiting.load(std::memory_order_relaxed)) return;
     if (d_.dead) {
       // a failed device only releases the jobs that name it
       std::unique_lock<std::mutex> lk(g_pool.mu);
@@ -504,8 +506,12 @@ void pool_start() {
   }
 }
 
+void pool_exit() {
+  g_exiting = true;
+  pool_stop();
+}
+
 void pool_stop() {
-  std::vector<JobP> pending;
   {
     std::lock_guard<std::mutex> g(g_pool.mu);
     g_pool.running = false;
