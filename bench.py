@@ -37,6 +37,11 @@ Other BASELINE.json configurations (``--workload``; not the driver's default lin
             (npow_submit), 25 % cancelled at uniform times in [0, 0.5 x the expected
             burst time); every reply re-validated on the CPU (libnanopow npow_work_value);
   sustained config 5: --duration seconds of back-to-back fresh roots, --depth in flight.
+  dpow      the MQTT path end to end: --roots work messages at
+            fffffff8 arriving as a Poisson stream at --rate per second, 25 % cancelled by
+            a cancel message, delivered to the WorkHandler-equivalent (nanopow.dpow,
+            --concurrency loops) -> HTTP work server -> engine -> result messages;
+            p50/p99 = work message -> result message (server/scripts/check_latency.py).
 """
 from __future__ import annotations
 
@@ -377,6 +382,71 @@ def workload_sustained(eng, args, rank, world, dist):
     return line
 
 
+def workload_dpow(eng, args, rank, world, dist):
+    """MQTT path: work/cancel messages -> WorkHandler-equivalent -> HTTP server -> results."""
+    import asyncio
+    import random
+    from nanopow import dpow
+    from nanopow.server import HttpWorkServer, WorkServer
+    n = args.roots
+    rng = random.Random(777 + rank)
+    srv = HttpWorkServer(WorkServer(eng, max_active=max(1, args.concurrency), device_mask=0 if world == 1 else 1),
+                         "127.0.0.1", 0).start()
+    hashes = [bench_root(11_000_000 + rank * 1_000_000 + i).hex().upper() for i in range(n)]
+    t, sched = 0.0, []
+    for h in hashes:
+        t += rng.expovariate(args.rate)
+        sched.append((t, "work/ondemand", f"{h},fffffff800000000".encode()))
+    cancelled = set(rng.sample(range(n), n // 4))
+    for i in cancelled:
+        sched.append((sched[i][0] + rng.uniform(0.0, 0.05), "cancel/ondemand", hashes[i].encode()))
+    published = []
+
+    async def main():
+        probe = dpow.LatencyProbe()
+
+        async def publish(topic, payload):
+            published.append((topic, payload))
+            probe.saw_result(topic, payload)
+        h = dpow.DpowWorkHandler(dpow.HttpWorker(srv.address, timeout=120), publish, "nano_bench",
+                                 concurrency=args.concurrency, rng=random.Random(rank))
+        await h.start()
+        wall = await dpow.replay(h, probe, sched, drain_timeout=300)
+        await h.stop()
+        return probe, wall
+    eng.reset_stats(0)
+    if dist is not None:
+        dist.barrier()
+    try:
+        probe, wall = asyncio.run(main())
+    finally:
+        srv.stop()
+    bad = 0
+    for _, payload in published:
+        bh, work, _ = payload.decode().split(",")
+        if eng.work_value(bytes.fromhex(bh), int(work, 16)) < SEND:
+            bad += 1
+    lat = [probe.latency[h] for h in probe.latency]
+    st = eng.stats(0) if world > 1 else None
+    if world == 1:
+        ks = [eng.stats(d) for d in range(eng.n_devices)]
+        kms, kn, nl = sum(k.kernel_ms for k in ks), sum(k.nonces for k in ks), sum(k.launches for k in ks)
+    else:
+        kms, kn, nl = st.kernel_ms, st.nonces, st.launches
+    nonces, wall, lat, (kms, kn, nl, n_bad) = _reduce(dist, kn, wall, lat, (kms, kn, nl, bad))
+    line = result_line(world, len(lat), 0, nonces, wall, lat or [0.0], kms, kn, nl)
+    line["config"] = {"workload": f"MQTT path end to end: {n} work messages per GPU at fffffff800000000, "
+                                  f"Poisson arrivals at {args.rate}/s, 25 % cancelled, WorkHandler-equivalent "
+                                  f"with {args.concurrency} loop(s) -> HTTP work server -> engine",
+                      "threshold": "fffffff800000000", "rate_per_s": args.rate, "concurrency": args.concurrency,
+                      "parallelism": f"dp{world}" if world > 1 else f"work pool over {eng.n_devices} GPU(s)"}
+    line["dpow"] = {"results": len(published), "cancelled": len(cancelled), "invalid_results": int(n_bad)}
+    line["value_note"] = "value = nonces hashed by the kernels / wall time of the whole message stream (idle included)"
+    if n_bad:
+        raise RuntimeError(f"dpow: {int(n_bad)} invalid results")
+    return line
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -384,11 +454,14 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--iters", type=int, default=0, help="override wave iterations per launch")
-    ap.add_argument("--workload", default="search", choices=["search", "allgpus", "sweep", "burst", "sustained"])
+    ap.add_argument("--workload", default="search",
+                    choices=["search", "allgpus", "sweep", "burst", "sustained", "dpow"])
     ap.add_argument("--sweep-bits", type=int, default=36, help="sweep: range [0, 2^bits)")
     ap.add_argument("--roots", type=int, default=4096, help="burst: requests per GPU")
     ap.add_argument("--duration", type=float, default=60.0, help="sustained: seconds")
     ap.add_argument("--depth", type=int, default=4, help="sustained: requests in flight per GPU")
+    ap.add_argument("--rate", type=float, default=20.0, help="dpow: work messages per second")
+    ap.add_argument("--concurrency", type=int, default=1, help="dpow: WorkHandler loops (reference: 1)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -405,7 +478,7 @@ def main() -> int:
     dev = 0
     if args.workload != "search":
         fn = {"allgpus": workload_allgpus, "sweep": workload_sweep, "burst": workload_burst,
-              "sustained": workload_sustained}[args.workload]
+              "sustained": workload_sustained, "dpow": workload_dpow}[args.workload]
         line = fn(eng, args, rank, WORLD, dist)
         if rank == 0:
             print(json.dumps(line), flush=True)

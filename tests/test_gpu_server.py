@@ -59,3 +59,45 @@ def test_send_difficulty_generate_and_validate(gpu_server):
 def test_benchmark_on_gpu(gpu_server):
     r = post(gpu_server.address, {"action": "benchmark", "count": 10})
     assert r["count"] == "10" and int(r["duration"]) > 0
+
+
+def test_dpow_messages_to_results_on_gpu(gpu_engine):
+    """MQTT-style work/cancel messages -> WorkHandler-equivalent (2 loops) -> HTTP work server ->
+    libnanopow -> result messages; every result re-validates under hashlib, cancelled hashes
+    publish nothing (client/dpow_client.py:38-39, 63-85; client/work_handler.py)."""
+    import asyncio
+    import random
+    from nanopow import dpow
+    srv = HttpWorkServer(WorkServer(gpu_engine, max_active=4), "127.0.0.1", 0).start()
+    rng = random.Random(21)
+    hashes = [bytes(rng.getrandbits(8) for _ in range(32)).hex().upper() for _ in range(24)]
+    sched = [(0.002 * i, "work/ondemand", f"{h},fffffe0000000000".encode()) for i, h in enumerate(hashes)]
+    never = [f"{0xEE00 + i:064X}" for i in range(3)]
+    sched += [(0.01, "work/precache", f"{h},ffffffffffffffff".encode()) for h in never]
+    sched += [(0.2, "cancel/precache", h.encode()) for h in never]
+    published = []
+
+    async def main():
+        probe = dpow.LatencyProbe()
+
+        async def publish(topic, payload):
+            published.append((topic, payload))
+            probe.saw_result(topic, payload)
+        h = dpow.DpowWorkHandler(dpow.HttpWorker(srv.address, timeout=60), publish, "nano_test", concurrency=4)
+        await h.start()
+        wall = await dpow.replay(h, probe, sched, drain_timeout=60)
+        await h.stop()
+        return probe, wall
+    try:
+        probe, wall = asyncio.run(main())
+    finally:
+        srv.stop()
+    assert wall < 30
+    got = {}
+    for topic, payload in published:
+        bh, work, acct = payload.decode().split(",")
+        assert topic == "result/ondemand" and acct == "nano_test"
+        assert oracle.work_value_hashlib(bytes.fromhex(bh), int(work, 16)) >= 0xfffffe0000000000
+        got[bh] = work
+    assert set(got) == set(hashes)
+    assert all(h not in probe.results for h in never)
