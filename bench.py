@@ -37,6 +37,9 @@ Other BASELINE.json configurations (``--workload``; not the driver's default lin
             (npow_submit), 25 % cancelled at uniform times in [0, 0.5 x the expected
             burst time); every reply re-validated on the CPU (libnanopow npow_work_value);
   sustained config 5: --duration seconds of back-to-back fresh roots, --depth in flight.
+  receive   config 1: single work_generate requests at receive difficulty fffffe0000000000,
+            on the GPU (C ABI and HTTP server) next to the reference's CPU path
+            (hashlib.blake2b, one core, and the oracle's C port on the host cores);
   dpow      the MQTT path end to end: --roots work messages at
             fffffff8 arriving as a Poisson stream at --rate per second, 25 % cancelled by
             a cancel message, delivered to the WorkHandler-equivalent (nanopow.dpow,
@@ -447,6 +450,83 @@ def workload_dpow(eng, args, rank, world, dist):
     return line
 
 
+def _hashlib_search(root: bytes, thr: int, start: int, limit: int):
+    """The reference's CPU path: hashlib.blake2b(digest_size=8) over consecutive nonces."""
+    b2 = hashlib.blake2b
+    n = start
+    for k in range(limit):
+        if int.from_bytes(b2(n.to_bytes(8, "little") + root, digest_size=8).digest(), "little") >= thr:
+            return k + 1, n
+        n = (n + 1) & ((1 << 64) - 1)
+    return limit, None
+
+
+def workload_receive(eng, args, rank, world, dist):
+    """BASELINE config 1: work_generate at fffffe0000000000, GPU next to the CPU reference."""
+    if world > 1:
+        raise SystemExit("--workload receive runs in one process")
+    recv = 0xfffffe0000000000
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle  # CPU baseline legs only
+    from nanopow.server import HttpWorkServer, WorkServer
+    import urllib.request
+    # GPU through the C ABI
+    gpu = []
+    for i in range(args.steps):
+        t = time.perf_counter()
+        r = eng.search(bench_root(20_000_000 + i), recv, start=bench_start(i), device_mask=0)
+        gpu.append(time.perf_counter() - t)
+        assert r.status == 0 and r.value >= recv
+    # GPU through the HTTP work server (what the DPoW client sees)
+    srv = HttpWorkServer(WorkServer(eng, max_active=1), "127.0.0.1", 0).start()
+    http = []
+    try:
+        for i in range(min(args.steps, 100)):
+            body = json.dumps({"action": "work_generate", "hash": bench_root(21_000_000 + i).hex(),
+                               "difficulty": f"{recv:016x}"}).encode()
+            t = time.perf_counter()
+            req = urllib.request.Request(f"http://{srv.address}", data=body, method="POST")
+            with urllib.request.urlopen(req, timeout=60) as resp:
+                rep = json.loads(resp.read())
+            http.append(time.perf_counter() - t)
+            assert "work" in rep
+    finally:
+        srv.stop()
+    # CPU: hashlib on one core (the reference's CPU path), a bounded number of requests
+    cpu1, cpu1_nonces = [], 0
+    for i in range(args.cpu_requests):
+        t = time.perf_counter()
+        k, nonce = _hashlib_search(bench_root(22_000_000 + i), recv, bench_start(i), 1 << 28)
+        cpu1.append(time.perf_counter() - t)
+        cpu1_nonces += k
+        assert nonce is not None
+    # CPU: the oracle's C port on the host cores (exhaustive scan of the same requests' first chunk)
+    threads = min(16, os.cpu_count() or 1)
+    cpun = []
+    for i in range(args.cpu_requests):
+        root = bench_root(22_000_000 + i)
+        t = time.perf_counter()
+        oracle.sweep(root, recv, bench_start(i), 1 << 24, threads=threads)  # 2x the expected nonces
+        cpun.append(time.perf_counter() - t)
+    line = result_line(1, args.steps, 0, 0, 1.0, gpu, 0.0, 0, 0)
+    line.pop("roofline")
+    line["value"] = round(pct(gpu, 50) * 1e3, 3)
+    line["unit"] = "ms p50 time-to-work (GPU, C ABI)"
+    line["higher_is_better"] = False
+    line["config"] = {"workload": "BASELINE configs[0]: single work_generate at receive difficulty "
+                                  "fffffe0000000000 (expected 2^23 nonces), GPU vs the CPU reference",
+                      "threshold": "fffffe0000000000"}
+    line["receive"] = {
+        "gpu_c_abi_ms": {"p50": round(pct(gpu, 50) * 1e3, 3), "p99": round(pct(gpu, 99) * 1e3, 3), "n": len(gpu)},
+        "gpu_http_ms": {"p50": round(pct(http, 50) * 1e3, 3), "p99": round(pct(http, 99) * 1e3, 3), "n": len(http)},
+        "cpu_hashlib_1core_ms": {"p50": round(pct(cpu1, 50) * 1e3, 1), "n": len(cpu1),
+                                 "gnps": round(cpu1_nonces / sum(cpu1) / 1e9, 6)},
+        "cpu_oracle_c_scan_2p24_ms": {"median": round(statistics.median(cpun) * 1e3, 1), "threads": threads,
+                                      "gnps": round((1 << 24) / statistics.median(cpun) / 1e9, 5)},
+    }
+    return line
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -455,13 +535,14 @@ def main() -> int:
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--iters", type=int, default=0, help="override wave iterations per launch")
     ap.add_argument("--workload", default="search",
-                    choices=["search", "allgpus", "sweep", "burst", "sustained", "dpow"])
+                    choices=["search", "allgpus", "sweep", "burst", "sustained", "dpow", "receive"])
     ap.add_argument("--sweep-bits", type=int, default=36, help="sweep: range [0, 2^bits)")
     ap.add_argument("--roots", type=int, default=4096, help="burst: requests per GPU")
     ap.add_argument("--duration", type=float, default=60.0, help="sustained: seconds")
     ap.add_argument("--depth", type=int, default=4, help="sustained: requests in flight per GPU")
     ap.add_argument("--rate", type=float, default=20.0, help="dpow: work messages per second")
     ap.add_argument("--concurrency", type=int, default=1, help="dpow: WorkHandler loops (reference: 1)")
+    ap.add_argument("--cpu-requests", type=int, default=4, help="receive: requests timed on the CPU reference")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -478,7 +559,7 @@ def main() -> int:
     dev = 0
     if args.workload != "search":
         fn = {"allgpus": workload_allgpus, "sweep": workload_sweep, "burst": workload_burst,
-              "sustained": workload_sustained, "dpow": workload_dpow}[args.workload]
+              "sustained": workload_sustained, "dpow": workload_dpow, "receive": workload_receive}[args.workload]
         line = fn(eng, args, rank, WORLD, dist)
         if rank == 0:
             print(json.dumps(line), flush=True)
