@@ -134,3 +134,61 @@ def test_batch_of_64_with_cancels(gpu_engine):
         assert x.status == _lib.NPOW_OK and oracle.work_value(r, x.nonce) == x.value >= RECEIVE
     assert all(x.status == _lib.NPOW_CANCELLED for x in res[48:])
     assert done > 0
+
+
+@pytest.mark.parametrize("count", [1, 63, 64, 65, 4095, (1 << 20) + 7])
+def test_bounded_ragged_counts_exhaust_exactly(gpu_engine, count):
+    """Ragged bounded ranges (partial last block, fewer blocks than waves) are hashed exactly
+    once, including a range that wraps 2^64 -> 0; several of them share the launch."""
+    starts = [0, 12345, M64 - count // 2]
+    ts = [gpu_engine.submit(bytes(range(32)), M64, start=s, device_mask=1, max_nonces_per_device=count)
+          for s in starts]
+    for t in ts:
+        r = t.wait(60)
+        assert r.status == _lib.NPOW_EXHAUSTED and r.nonces_done == count
+
+
+def test_bounded_first_hit_in_ragged_ranges(gpu_engine):
+    """Threshold 0 makes every nonce a hit: the winner of a bounded range must lie inside it,
+    for ragged lengths and a range across 2^64; an exact-value threshold finds exactly that nonce."""
+    root = bytes(range(7, 39))
+    for start, count in [(M64 - 2, 5), (1000, 1), (77, 65)]:
+        r = gpu_engine.submit(root, 0, start=start, device_mask=1, max_nonces_per_device=count).wait(60)
+        assert r.status == _lib.NPOW_OK
+        assert (r.nonce - start) & M64 < count and r.value == oracle.work_value(root, r.nonce)
+    vals = gpu_engine.values(root, 5000, 3000)
+    top = max(range(3000), key=lambda i: vals[i])
+    r = gpu_engine.submit(root, vals[top], start=5000, device_mask=1, max_nonces_per_device=3000).wait(60)
+    assert r.status == _lib.NPOW_OK and r.nonce == 5000 + top and r.value == vals[top]
+    r = gpu_engine.submit(root, vals[top] + 1, start=5000, device_mask=1, max_nonces_per_device=3000).wait(60)
+    assert r.status == _lib.NPOW_EXHAUSTED and r.nonces_done == 3000
+
+
+def test_duplicate_roots_in_flight_are_independent_jobs(gpu_engine):
+    """The same root submitted several times at once (a collision in the burst): every ticket
+    gets its own valid answer; cancelling one leaves the others running to completion."""
+    root = bytes(range(100, 132))
+    toks = [_lib.CancelToken() for _ in range(6)]
+    ts = [gpu_engine.submit(root, RECEIVE, start=i << 58, device_mask=1, cancel=toks[i]) for i in range(6)]
+    toks[2].set()
+    for i, t in enumerate(ts):
+        r = t.wait(60)
+        if i == 2 and r.status == _lib.NPOW_CANCELLED:
+            continue
+        assert r.status == _lib.NPOW_OK and oracle.work_value(root, r.nonce) == r.value >= RECEIVE
+
+
+def test_full_table_of_64_bounded_and_unbounded(gpu_engine):
+    """64 live entries (the table's maximum): 32 bounded no-hit ranges of ragged sizes next to
+    32 unbounded searches; exact exhaustion counts and valid winners."""
+    roots = _roots(17, 64)
+    counts = [1 + 977 * i for i in range(32)]
+    bt = [gpu_engine.submit(r, M64, start=i << 40, device_mask=1, max_nonces_per_device=c)
+          for i, (r, c) in enumerate(zip(roots[:32], counts))]
+    ut = [gpu_engine.submit(r, LOW, device_mask=1) for r in roots[32:]]
+    for c, t in zip(counts, bt):
+        r = t.wait(60)
+        assert r.status == _lib.NPOW_EXHAUSTED and r.nonces_done == c
+    for root, t in zip(roots[32:], ut):
+        r = t.wait(60)
+        assert r.status == _lib.NPOW_OK and oracle.work_value(root, r.nonce) == r.value >= LOW

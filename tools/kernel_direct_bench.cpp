@@ -5,7 +5,7 @@
 //   pool8 = npow_pool_kernel<false> with eight unbounded entries
 // Build: hipcc -O3 --offload-arch=gfx950 -Inano-dpow_amd/csrc -Iinclude -x hip tools/kernel_direct_bench.cpp
 //        -x none nano-dpow_amd/csrc/npow_kernel.o -o build/kernel_direct_bench
-// Run:   ./build/kernel_direct_bench [reps] [iters]
+// Run:   ./build/kernel_direct_bench [reps] [iters] [poll_mask]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -29,6 +29,7 @@ using namespace npow;
 int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
   const uint32_t iters = argc > 2 ? (uint32_t)atoi(argv[2]) : 256;
+  const uint32_t pmask = argc > 3 ? (uint32_t)atoi(argv[3]) : 1023;  // host-word poll mask
   CK(hipSetDevice(0));
   hipDeviceProp_t p;
   CK(hipGetDeviceProperties(&p, 0));
@@ -59,7 +60,7 @@ int main(int argc, char** argv) {
   LaunchArgs a{};
   fill_uniforms(a, pre);
   a.threshold = ~0ull;
-  a.poll_mask = 1023;
+  a.poll_mask = pmask;
   a.count = W * 64 * iters;
 
   PoolTable* tabs[2];
@@ -67,7 +68,7 @@ int main(int argc, char** argv) {
     PoolTable h{};
     const uint32_t n = k == 0 ? 1 : 8;
     h.n = n;
-    h.poll_mask = 1023;
+    h.poll_mask = pmask;
     h.iters = iters;
     for (uint32_t e = 0; e < n; ++e) {
       npow_asm_uniforms(pre.m, h.e[e].u);
