@@ -13,7 +13,7 @@ import subprocess
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 
-PATTERNS = {
+PATTERNS_ALL = {
     "xor": ["xor"],
     "align": ["align"],
     "add64": ["add64"],
@@ -37,6 +37,28 @@ PATTERNS = {
     "G-like grouped": ["xor", "xor", "xor", "xor", "xor", "xor", "xor", "xor", "lshr", "align", "align", "align",
                        "align", "add64", "add64", "add64", "add64", "add64"],
 }
+PATTERNS_SDWA = {
+    "mov": ["mov"],
+    "movsdwa": ["movsdwa"],
+    "mov|align alt": ["mov", "align"],
+    "movsdwa|align alt": ["movsdwa", "align"],
+    "movsdwa|add64 alt": ["movsdwa", "add64"],
+    "mov|add64 alt": ["mov", "add64"],
+    "mov|xor alt": ["mov", "xor"],
+    "not|align alt": ["not", "align"],
+    "mov64|align alt": ["mov64", "align"],
+    "movdpp|align alt": ["movdpp", "align"],
+    "xorsdwa|align alt": ["xorsdwa", "align"],
+    "lshr movsdwa|align align": ["lshr", "movsdwa", "align", "align"],
+    "G rot16 by align": ["xor", "xor", "align", "align", "add64", "xor", "xor", "add64", "xor", "xor", "align", "align",
+                         "add64", "xor", "xor", "lshr", "add64", "add64"],
+    "G rot16 by lshr+movsdwa": ["xor", "xor", "align", "align", "add64", "xor", "xor", "add64", "xor", "xor", "lshr",
+                                "movsdwa", "lshr", "movsdwa", "add64", "xor", "xor", "lshr", "add64", "add64"],
+    "G rot16 by mov-pair (upper bound)": ["xor", "xor", "align", "align", "add64", "xor", "xor", "add64", "xor", "xor",
+                                          "lshr", "mov", "lshr", "mov", "add64", "xor", "xor", "lshr", "add64", "add64"],
+}
+import os as _os
+PATTERNS = PATTERNS_SDWA if _os.environ.get("MIX_SET") == "sdwa" else PATTERNS_ALL
 
 
 def emit(kind, i):
@@ -59,13 +81,23 @@ def emit(kind, i):
         return f"v_mov_b32 v{d}, v{s0}"
     if kind == "perm":
         return f"v_perm_b32 v{d}, v{s0}, v{s1}, v{s1 + 1}"
+    if kind == "movsdwa":
+        return f"v_mov_b32_sdwa v{d}, v{s0} dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0"
+    if kind == "xorsdwa":
+        return f"v_xor_b32_sdwa v{d}, v{s0}, v{s1} dst_sel:WORD_1 dst_unused:UNUSED_PRESERVE src0_sel:WORD_0 src1_sel:WORD_0"
+    if kind == "not":
+        return f"v_not_b32 v{d}, v{s0}"
+    if kind == "mov64":
+        return f"v_mov_b64 v[{d}:{d + 1}], v[{s0}:{s0 + 1}]"
+    if kind == "movdpp":
+        return f"v_mov_b32_dpp v{d}, v{s0} quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf"
     if kind == "bitop3":
         return f"v_bitop3_b32 v{d}, v{s0}, v{s1}, v{s1 + 1} bitop3:0x96"
     raise ValueError(kind)
 
 
 def main():
-    n_body = 72  # instructions per asm block (a multiple of every pattern length used)
+    n_body = 360  # instructions per asm block (a multiple of every pattern length used: 1,2,3,4,18,20)
     kernels, runs, names = [], [], []
     clob = ", ".join(f'"v{r}"' for r in range(8, 64))
     for k, (name, pat) in enumerate(PATTERNS.items()):
