@@ -133,7 +133,7 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
                  const volatile uint32_t* cancel, std::vector<uint64_t>& hits, uint64_t& n_total,
                  bool& cancelled) {
   std::lock_guard<std::mutex> lk(d.mu);
-  HIPTRY(hipSetDevice(d.id));
+  HIPTRY(hipSetDevice(d.hip_id));
   int rc = reset_task(d);
   if (rc) return rc;
   LaunchArgs a{};
@@ -205,12 +205,21 @@ int npow_init(int* n_devices) {
   hipError_t e = hipGetDeviceCount(&n);
   if (e != hipSuccess || n <= 0)
     return fail(NPOW_ERR_NO_DEVICE, std::string("no HIP device: ") + hipGetErrorString(e));
-  for (int i = 0; i < n && i < 64; ++i) {
+  // NANOPOW_VIRTUAL_DEVICES=N (testing): expose N logical devices over the physical ones
+  // (logical i -> HIP device i mod n), each with its own stream, buffers and pool worker, so
+  // the multi-device first-win path runs on a one-GPU machine.
+  int n_logical = n;
+  if (const char* v = getenv("NANOPOW_VIRTUAL_DEVICES")) {
+    const int k = atoi(v);
+    if (k > 0) n_logical = k;
+  }
+  for (int i = 0; i < n_logical && i < 64; ++i) {
     auto d = std::make_unique<Device>();
     d->id = i;
-    HIPTRY(hipSetDevice(i));
+    d->hip_id = i % n;
+    HIPTRY(hipSetDevice(d->hip_id));
     hipDeviceProp_t p;
-    HIPTRY(hipGetDeviceProperties(&p, i));
+    HIPTRY(hipGetDeviceProperties(&p, d->hip_id));
     d->cus = p.multiProcessorCount;
     HIPTRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
     HIPTRY(hipMalloc(&d->st, sizeof(DevState)));
@@ -251,7 +260,7 @@ void npow_shutdown(void) {
   if (g_init) pool_stop();
   for (auto& d : g_devs) {
     std::lock_guard<std::mutex> lk(d->mu);
-    (void)hipSetDevice(d->id);
+    (void)hipSetDevice(d->hip_id);
     (void)hipStreamSynchronize(d->stream);
     for (int r = 0; r < kEventRing; ++r) {
       (void)hipEventDestroy(d->ev_start[r]);
@@ -448,7 +457,7 @@ int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t cou
     return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
   Device& d = *g_devs[device];
   std::lock_guard<std::mutex> lk(d.mu);
-  HIPTRY(hipSetDevice(d.id));
+  HIPTRY(hipSetDevice(d.hip_id));
   int rc = reset_task(d);
   if (rc) return rc;
   LaunchArgs a{};
@@ -475,7 +484,7 @@ int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, 
   if (n == 0) return NPOW_OK;
   Device& d = *g_devs[device];
   std::lock_guard<std::mutex> lk(d.mu);
-  HIPTRY(hipSetDevice(d.id));
+  HIPTRY(hipSetDevice(d.hip_id));
   std::vector<uint64_t> words((size_t)n * 4);
   for (uint32_t i = 0; i < n; ++i)
     for (int k = 0; k < 4; ++k) words[4 * (size_t)i + k] = host_load_le64(roots + 32 * (size_t)i + 8 * k);

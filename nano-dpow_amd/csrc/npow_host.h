@@ -30,7 +30,8 @@ const std::string& last_error();
 constexpr int kEventRing = 4;
 
 struct Device {
-  int id = 0;
+  int id = 0;       // logical index (device_mask bit)
+  int hip_id = 0;   // HIP device (== id unless NANOPOW_VIRTUAL_DEVICES is set)
   int cus = 0;
   hipStream_t stream = nullptr;
   DevState* st = nullptr;        // device memory (sweep / values tasks)

@@ -419,7 +419,7 @@ int Worker::step() {
 }
 
 void Worker::run() {
-  if (hipSetDevice(d_.id) != hipSuccess) d_.dead = true;
+  if (hipSetDevice(d_.hip_id) != hipSuccess) d_.dead = true;
   for (;;) {
     if (g_exiting.load(std::memory_order_relaxed)) return;
     if (d_.dead) {

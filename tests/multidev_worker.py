@@ -1,0 +1,87 @@
+"""Child process of tests/test_gpu_multidevice.py (run with NANOPOW_VIRTUAL_DEVICES=4): the
+multi-device first-win path on one physical GPU exposed as 4 logical devices, each with its own
+stream, buffers and pool worker.  Prints one JSON line; exits non-zero on any mismatch."""
+import json
+import os
+import random
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "nano-dpow_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import oracle  # noqa: E402  (the checker)
+from nanopow import _lib  # noqa: E402
+
+M64 = (1 << 64) - 1
+RECEIVE, LOW = 0xfffffe0000000000, 0xfffff00000000000
+
+
+def main():
+    eng = _lib.Engine()
+    G = eng.n_devices
+    assert G == int(os.environ["NANOPOW_VIRTUAL_DEVICES"]), G
+    out = {"devices": G}
+    spacing = (1 << 64) // G
+    for d in range(G):
+        eng.reset_stats(d)
+    # 1. searches over every device: valid winners, every device launched
+    rng = random.Random(3)
+    for _ in range(16):
+        root = bytes(rng.getrandbits(8) for _ in range(32))
+        r = eng.search(root, RECEIVE, start=rng.getrandbits(64), device_mask=0)
+        assert r.status == _lib.NPOW_OK and oracle.work_value_hashlib(root, r.nonce) == r.value >= RECEIVE
+    launches = [eng.stats(d).launches for d in range(G)]
+    assert all(x > 0 for x in launches), launches
+    out["launches_per_device"] = launches
+    # 2. exhaustion: each device hashes exactly its own bounded stride
+    r = eng.search(bytes(32), M64, start=12345, device_mask=0, max_nonces_per_device=100_003)
+    assert r.status == _lib.NPOW_EXHAUSTED and r.nonces_done == G * 100_003, r
+    # 3. the winner comes from the stride that holds the only hit: device 2's first nonce has a
+    #    high value; every device hashes exactly one nonce at threshold = that value
+    root = bytes(range(50, 82))
+    base = 777
+    x = None
+    for i in range(1 << 20):
+        n = (base + 2 * spacing + i) & M64
+        if oracle.work_value(root, n) >= 0xffff000000000000:
+            x = n
+            break
+    assert x is not None
+    vx = oracle.work_value(root, x)
+    start = (x - 2 * spacing) & M64
+    others = [oracle.work_value(root, (start + k * spacing) & M64) for k in range(G) if k != 2]
+    assert all(v < vx for v in others)
+    r = eng.search(root, vx, start=start, device_mask=0, max_nonces_per_device=1)
+    assert r.status == _lib.NPOW_OK and r.nonce == x and r.value == vx, (r, x)
+    # 4. cancellation reaches every device
+    tok = _lib.CancelToken()
+    t = eng.submit(bytes(range(32)), M64, device_mask=0, cancel=tok)
+    assert t.wait(0.2) is None
+    tok.set()
+    r = t.wait(30)
+    assert r.status == _lib.NPOW_CANCELLED and r.nonces_done > 0
+    # 5. a burst of jobs, each over every device
+    roots = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(48)]
+    ts = [eng.submit(rt, LOW, start=rng.getrandbits(64), device_mask=0) for rt in roots]
+    for rt, t in zip(roots, ts):
+        r = t.wait(60)
+        assert r.status == _lib.NPOW_OK and oracle.work_value(rt, r.nonce) == r.value >= LOW
+    # 6. a sweep split over the devices is exact
+    sroot = bytes(range(9, 41))
+    hits = eng.sweep(sroot, 0xffff000000000000, 1 << 40, (1 << 22) + 13, device_mask=0)
+    assert hits == oracle.sweep(sroot, 0xffff000000000000, 1 << 40, (1 << 22) + 13)
+    # 7. a subset mask: devices 1 and 3 only
+    for d in range(G):
+        eng.reset_stats(d)
+    r = eng.search(bytes(range(1, 33)), RECEIVE, device_mask=0b1010)
+    assert r.status == _lib.NPOW_OK
+    used = [eng.stats(d).launches > 0 for d in range(G)]
+    assert used == [False, True, False, True], used
+    out["ok"] = True
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
