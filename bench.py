@@ -148,6 +148,17 @@ def run_timed(search, stats, reset_stats, steps: int, warmup: int, rank: int, wo
     return int(v[0]), float(w_t[0]), all_ttw, float(v[1]), int(v[2]), int(v[3])
 
 
+def _pmc_traffic():
+    """HBM bytes per npow_pool_kernel launch measured by rocprofv3 PMC passes (tools/pmc_pool.sh on
+    this bench's workload; FETCH_SIZE doubled per the gfx950 correction).  PMC needs the profiler
+    around the process, so the bench reports the committed measurement; None if absent."""
+    try:
+        with open(os.path.join(HERE, "profiles", "r01_pmc_pool.json")) as f:
+            return json.load(f)["hbm_bytes_per_launch"]
+    except (OSError, ValueError, KeyError):
+        return None
+
+
 def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, kern_nonces, launches):
     gnps = tot_nonces / max_wall / 1e9
     per_rank_kernel_s = kern_ms * 1e-3 / world
@@ -183,7 +194,9 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
             "peak": round(PEAK_TOPS, 3),
             "unit": "Tops/s (int32 VALU)",
             "frac": round(achieved / PEAK_TOPS, 4),
-            "traffic": None,
+            "traffic": _pmc_traffic(),
+            "traffic_unit": "HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
+                            "(profiles/r01_pmc_pool.json, tools/pmc_pool.sh); algorithmic bytes: 0",
             "ops_per_nonce": OPS_PER_NONCE,
             "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
             "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
