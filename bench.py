@@ -547,6 +547,8 @@ def main() -> int:
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--iters", type=int, default=0, help="override wave iterations per launch")
+    ap.add_argument("--budget-us", type=int, default=-1, help="override the search launch budget (0 = off)")
+    ap.add_argument("--pool-blocks", type=int, default=0, help="override search workgroups per CU")
     ap.add_argument("--workload", default="search",
                     choices=["search", "allgpus", "sweep", "burst", "sustained", "dpow", "receive"])
     ap.add_argument("--sweep-bits", type=int, default=36, help="sweep: range [0, 2^bits)")
@@ -569,6 +571,8 @@ def main() -> int:
     eng = nanopow.engine()  # fails loudly without libnanopow.so / a GPU: no CPU fallback
     if args.iters:
         eng.set_tuning(args.iters, 0, 0)
+    if args.budget_us >= 0 or args.pool_blocks:
+        eng.set_pool_tuning(None if args.budget_us < 0 else args.budget_us, args.pool_blocks)
     dev = 0
     if args.workload != "search":
         fn = {"allgpus": workload_allgpus, "sweep": workload_sweep, "burst": workload_burst,

@@ -157,6 +157,16 @@ int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, 
  * blocks_per_cu: workgroups of 256 lanes per CU in the launch grid. */
 int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t blocks_per_cu);
 
+/* Search (work pool) launches.  budget_us: wall-clock budget of a launch (default 20000;
+ * 0 = iteration count only; 0xffffffff keeps the current value).  Waves searching unbounded
+ * jobs stop together when it runs out -- VALU issue favours a SIMD's oldest wave, so a launch
+ * of a fixed iteration count ends in a tail of one or two waves per SIMD -- and
+ * iters_per_launch (default 8192) is then only the cap (and the span of bounded jobs, which
+ * always complete their dense ranges).  A running launch is ended early when new jobs arrive
+ * for its device.  blocks_per_cu: workgroups per CU of a search launch (default 4; 0 keeps).
+ * npow_set_tuning's blocks_per_cu applies to sweeps and value ranges. */
+int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu);
+
 int npow_device_stats_get(int device, npow_device_stats* out);
 int npow_device_stats_reset(int device);
 

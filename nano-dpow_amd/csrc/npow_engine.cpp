@@ -43,9 +43,17 @@ int fail(int code, const std::string& msg) {
 const std::string& last_error() { return t_err; }
 
 std::vector<std::unique_ptr<Device>> g_devs;
-std::atomic<uint32_t> g_iters{256};     // wave iterations per launch (2^27 nonces at 2048 x 256 lanes)
+std::atomic<uint32_t> g_iters{8192};    // search launches: iteration cap under the time budget (the oldest wave of a
+                                        // SIMD runs ~4 us per iteration, ~5,000 in 20 ms) and the span of bounded jobs
+constexpr uint32_t kSweepIters = 512;   // sweep launches: wave iterations (2^28 nonces, ~10 ms)
 std::atomic<uint32_t> g_poll{1024};     // a wave reads the host word every g_poll iterations (8 waves per iteration grid-wide)
 std::atomic<uint32_t> g_blocks_per_cu{8};
+std::atomic<uint32_t> g_budget_us{20000};  // pool launches end on time, not on their slowest wave
+// Pool launches: 4 workgroups (16 waves) per CU.  Four waves per SIMD already saturate VALU
+// issue under the time budget (27.05 Gnonce/s at 4, 5 and 6 per CU), and the pool kernel's
+// ~100 SGPRs admit only 6 per CU (tools/wave_probe.cpp: with 8 requested, 2 per CU start
+// only when the first 6 finish), so 4 leaves room for compiler changes.
+std::atomic<uint32_t> g_pool_blocks_per_cu{4};
 
 std::vector<Device*> select_devices(uint64_t mask) {
   std::vector<Device*> out;
@@ -141,7 +149,7 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
   a.threshold = threshold;
   a.poll_mask = poll_mask();
   a.cap = (uint32_t)kHitCap;
-  const uint64_t chunk = (uint64_t)grid_of(d) * kBlock * g_iters.load();
+  const uint64_t chunk = (uint64_t)grid_of(d) * kBlock * kSweepIters;
   uint64_t issued = 0;
   int ring = 0;
   std::deque<Inflight> q;
@@ -295,6 +303,14 @@ int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t 
   return NPOW_OK;
 }
 
+int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu) {
+  if (budget_us != 0xffffffffu && budget_us > 1000000) return fail(NPOW_ERR_BAD_ARGUMENT, "budget_us must be <= 1000000");
+  if (blocks_per_cu > 32) return fail(NPOW_ERR_BAD_ARGUMENT, "blocks_per_cu must be <= 32");
+  if (budget_us != 0xffffffffu) g_budget_us = budget_us;
+  if (blocks_per_cu) g_pool_blocks_per_cu = blocks_per_cu;
+  return NPOW_OK;
+}
+
 int npow_device_stats_get(int device, npow_device_stats* out) {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size() || !out) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
@@ -305,7 +321,7 @@ int npow_device_stats_get(int device, npow_device_stats* out) {
   out->kernel_ms = d.kernel_ms;
   out->invalid_work = d.invalid;
   out->cus = d.cus;
-  out->grid = grid_of(d);
+  out->grid = pool_grid_of(d);
   return NPOW_OK;
 }
 

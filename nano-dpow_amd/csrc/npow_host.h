@@ -61,8 +61,11 @@ extern std::vector<std::unique_ptr<Device>> g_devs;
 extern std::atomic<uint32_t> g_iters;          // wave iterations per launch
 extern std::atomic<uint32_t> g_poll;           // host-word poll interval (iterations per wave)
 extern std::atomic<uint32_t> g_blocks_per_cu;  // workgroups per CU
+extern std::atomic<uint32_t> g_budget_us;      // pool launches: wall-clock budget per wave (0 = off)
+extern std::atomic<uint32_t> g_pool_blocks_per_cu;  // pool launches: workgroups per CU
 
-inline int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }
+inline int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }        // sweep / values
+inline int pool_grid_of(const Device& d) { return d.cus * (int)g_pool_blocks_per_cu.load(); }  // searches
 inline uint32_t poll_mask() {
   uint32_t p = g_poll.load();
   uint32_t m = 1;

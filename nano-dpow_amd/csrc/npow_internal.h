@@ -95,8 +95,13 @@ struct PoolEntry {
 struct PoolTable {
   uint32_t n;          // entries in use (1..kMaxSlots)
   uint32_t poll_mask;  // a wave reads the host kill word when ((it + w) & poll_mask) == 0
-  uint32_t iters;      // wave iterations of this launch
-  uint32_t pad[13];
+  uint32_t iters;      // wave iterations of this launch (the cap; bounded entries' dense span)
+  uint32_t budget;     // > 0: a wave on an unbounded entry stops once this many 100-MHz
+                       // s_memrealtime ticks have passed since it started (all waves stop
+                       // together); 0 = iteration count only
+  uint64_t yield_base;    // PoolMailbox::yield when the table was built: a polling wave that
+                          // reads a different value ends the launch's unbounded entries
+  uint32_t pad[10];
   PoolEntry e[kMaxSlots];
 };
 inline size_t pool_table_bytes(uint32_t n) { return offsetof(PoolTable, e) + (size_t)n * sizeof(PoolEntry); }
@@ -121,6 +126,7 @@ struct alignas(64) PoolWin {
 struct PoolMailbox {
   PoolWin win[kMaxSlots];
   uint64_t kill[kMaxSlots];  // kill[s] = gen: the job in slot s (that generation) must stop
+  alignas(64) uint64_t yield;  // bumped by the host when new jobs wait for the next launch
 };
 
 // Launchers (defined in npow_kernel.hip).

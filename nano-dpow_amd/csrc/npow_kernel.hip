@@ -182,6 +182,10 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
 // cancelled, or its bounded range is used up) the wave moves to the next live unbounded
 // entry instead of idling for the rest of the launch.  Index mapping: PoolEntry comment in
 // npow_internal.h.  With one entry this is the plain first-win search.
+#ifdef NPOW_WAVE_PROBE
+__device__ uint64_t npow_wave_probe[32768 * 4];
+#endif
+
 struct PoolCursor {
   uint64_t u[NPOW_ASM_N_UNIFORMS];
   uint64_t threshold, base, gen;
@@ -190,6 +194,7 @@ struct PoolCursor {
   uint32_t it_end;    // the wave runs the entry while it < it_end
   uint32_t last_b;    // bounded: index of the entry's last block ...
   uint32_t tail;      // ... and its lanes in range (64 = full)
+  uint32_t bounded;   // exact dense coverage: ignores the launch's time budget
 };
 
 // Load entry `pe` into the cursor for wave w.  own: the entry's own waves (w % n == e) --
@@ -202,6 +207,7 @@ __device__ __forceinline__ void pool_load(const PoolEntry* __restrict__ pe, Pool
   c.base = pe->base;
   c.gen = pe->gen;
   c.slot = pe->slot;
+  c.bounded = pe->bounded;
   if (pe->bounded) {
     // own waves only (migrants never pick a bounded entry); count <= K * iters * 64 < 2^32 * 64
     c.K = W / n + (e < W % n ? 1u : 0u);
@@ -226,21 +232,39 @@ __device__ __forceinline__ uint64_t load_dead(PoolDevState* st, uint32_t slot) {
 
 // BOUNDED: the table holds at least one bounded entry (partial last blocks need a per-lane
 // range test); the plain search (every entry unbounded) compiles without it.
+#ifndef NPOW_POOL_NUM_SGPR
+#define NPOW_POOL_NUM_SGPR 0
+#endif
 template <bool BOUNDED>
-__global__ __launch_bounds__(kBlock) void npow_pool_kernel(const PoolTable* __restrict__ tab,
+__global__ __launch_bounds__(kBlock)
+#if NPOW_POOL_NUM_SGPR
+__attribute__((amdgpu_num_sgpr(NPOW_POOL_NUM_SGPR)))
+#endif
+void npow_pool_kernel(const PoolTable* __restrict__ tab,
                                                            PoolDevState* __restrict__ st,
                                                            PoolMailbox* __restrict__ mb) {
+  uint64_t t_start;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
   const uint32_t W = gridDim.x * (kBlock / 64);
-  const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask;
+  const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask, budget = tab->budget;
   unsigned long long* const done_base = &st->done[0][(blockIdx.x % kPoolDoneShards) * 8];
+  // Time budget.  VALU issue on a SIMD goes to its OLDEST wave first (MI355X_MICROARCH.md:
+  // priority, then age), so the 8 waves of a SIMD do not progress together: the oldest runs
+  // at single-wave speed and finishes first, the youngest barely runs until the others are
+  // done (tools/wave_probe.cpp: wave finish times 1.0 - 5.6 ms in a 5.6-ms launch).  A launch
+  // of a fixed iteration count therefore ends in a tail where one or two waves per SIMD are
+  // left.  Unbounded entries need no fixed partition, so every wave instead stops at the same
+  // wall-clock point, its own start (read first thing, before any VALU instruction the age
+  // arbitration could hold back) + budget; region holes are unused nonces.
 
   uint32_t e = w % n;
   PoolCursor c;
   pool_load(&tab->e[e], c, true, w, W, n, e, iters);
 
   uint32_t it = 0;
+  bool out_of_time = false;
   for (;;) {
     uint32_t done = 0;  // nonces this wave hashed for the current entry (<= iters * 64)
     while (it < c.it_end) {
@@ -250,10 +274,13 @@ __global__ __launch_bounds__(kBlock) void npow_pool_kernel(const PoolTable* __re
 #define NPOW_POOL_POLL 3
 #endif
       const uint64_t dead = (NPOW_POOL_POLL & 1) ? load_dead(st, c.slot) : 0;
-      uint64_t kill = 0;
-      if ((NPOW_POOL_POLL & 2) && ((it + w) & poll_mask) == 0)
+      uint64_t kill = 0, yld = tab->yield_base;
+      if ((NPOW_POOL_POLL & 2) && ((it + w) & poll_mask) == 0) {
         kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        yld = __hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
 
+      const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;  // consumed after the hash
       const uint32_t b = it * c.K + c.j;  // < 2^31: the entry's blocks of this launch
       const uint64_t nonce = c.base + ((uint64_t)b << 6) + lane;
       const uint64_t value = npow_asm_work_value(nonce, c.u);
@@ -280,14 +307,26 @@ __global__ __launch_bounds__(kBlock) void npow_pool_kernel(const PoolTable* __re
         }
         break;
       }
+      if (__builtin_expect(readlane64(yld, 0) != tab->yield_base, 0)) {
+        // the host has new jobs for this device: end every unbounded entry of this launch
+        // (their jobs come back in the next launch's table with new generations)
+        if (lane == 0)
+          for (uint32_t k = 0; k < n; ++k)
+            if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
+        if (!c.bounded) break;
+      }
       if (readlane64(kill, 0) == c.gen) {  // generations only grow: == is "this job"
         if (lane == 0) atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen);  // relay
         break;
       }
       if (readlane64(dead, 0) == c.gen) break;
+      if (budget && !c.bounded && now - t_start >= budget) {  // out of time: the wave is done
+        out_of_time = true;
+        break;
+      }
     }
     if (lane == 0 && done) atomicAdd(done_base + (size_t)c.slot * (kPoolDoneShards * 8), (unsigned long long)done);
-    if (it >= iters) break;
+    if (it >= iters || out_of_time) break;
     // the entry died or its bounded range is used up: next live unbounded entry (cyclic
     // from e + 1); none left -> the wave is finished
     uint32_t next = n;
@@ -304,6 +343,16 @@ __global__ __launch_bounds__(kBlock) void npow_pool_kernel(const PoolTable* __re
     e = next;
     pool_load(&tab->e[e], c, false, w, W, n, e, iters);
   }
+#ifdef NPOW_WAVE_PROBE
+  // diagnostic build (tools/wave_probe.cpp): per-wave start / end realtime, iterations, HW ids
+  if (lane == 0) {
+    npow_wave_probe[w * 4 + 0] = t_start;
+    npow_wave_probe[w * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    npow_wave_probe[w * 4 + 2] = it;
+    npow_wave_probe[w * 4 + 3] = ((uint64_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |  // XCC_ID
+                                 (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));         // HW_ID
+  }
+#endif
 }
 
 hipError_t launch_pool(int grid, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,

@@ -40,6 +40,7 @@ namespace npow {
 namespace {
 
 constexpr int kPending = 100;  // job status before it is decided
+constexpr double kYieldMinUs = 1500.0;  // yield a running launch only if more budget than this is left
 
 struct Job {
   uint64_t ticket = 0;
@@ -145,6 +146,7 @@ struct Slot {
   bool requeue = false;    // invalid GPU result: hand the job back to this device after retiring
   bool no_more = false;    // bounded range fully issued
   bool readback = false;   // done-shard read-back queued (ev_done[slot] marks it)
+  bool fresh = false;      // adopted since the last launch was built
 };
 
 struct PoolInflight {
@@ -164,6 +166,8 @@ class Worker {
   uint64_t seq_ = 0;  // launches issued by this worker
   uint64_t seen_version_ = ~0ull;
   int ring_ = 0;
+  std::chrono::steady_clock::time_point front_start_{};  // host estimate of the running launch's start
+  uint64_t yields_ = 0;
   std::unique_lock<std::mutex> dev_lock_{d_.mu, std::defer_lock};
 
   bool busy() const {
@@ -173,6 +177,7 @@ class Worker {
     return false;
   }
   void adopt();
+  void yield_if_long();
   void handle_win(int s);
   bool win_published(int s) const;
   void check_slots();
@@ -201,6 +206,7 @@ bool wants_device_locked(int dev) {
 void Worker::adopt() {
   const uint64_t v = g_pool.version.load();
   if (v == seen_version_) return;
+  bool adopted = false;
   std::lock_guard<std::mutex> g(g_pool.mu);
   seen_version_ = g_pool.version.load();
   for (const JobP& j : std::vector<JobP>(g_pool.active)) {  // copy: device_done_locked may erase
@@ -222,7 +228,33 @@ void Worker::adopt() {
     sl.k = (size_t)k;
     sl.gen = ++g_gen;
     sl.win_seen = sl.requeue = sl.no_more = sl.readback = false;
+    sl.fresh = true;
     j->on_dev[k] = 1;
+    adopted = true;
+  }
+  if (adopted) yield_if_long();
+}
+
+// New jobs wait for the next launch's table.  Launches run for a long time budget (their
+// start costs ~0.1-0.2 ms of cold instruction/scalar caches, so long launches are faster), so
+// when the running launch still has a while to go, end its unbounded entries now: bump the
+// pinned yield word (polling waves mark those entries dead) and hand their jobs back for
+// re-adoption with new generations next to the new ones.
+void Worker::yield_if_long() {
+  if (q_.empty() || g_budget_us.load() == 0) return;
+  const double left_us = g_budget_us.load() - std::chrono::duration<double, std::micro>(
+                                                  std::chrono::steady_clock::now() - front_start_).count();
+  if (q_.size() < 2 && left_us < kYieldMinUs) return;
+  bool any = false;
+  for (Slot& sl : slots_) {
+    if (sl.state != SlotState::kActive || sl.fresh || sl.job->max_per_dev) continue;
+    sl.requeue = true;
+    sl.state = SlotState::kDraining;
+    any = true;
+  }
+  if (any) {
+    __atomic_store_n(&d_.pmb->yield, __atomic_load_n(&d_.pmb->yield, __ATOMIC_RELAXED) + 1, __ATOMIC_RELEASE);
+    ++yields_;
   }
 }
 
@@ -287,7 +319,7 @@ void Worker::check_slots() {
 int Worker::launch() {
   if (q_.size() >= 2) return NPOW_OK;
   const uint32_t iters = g_iters.load();
-  const uint32_t W = (uint32_t)grid_of(d_) * (kBlock / 64);
+  const uint32_t W = (uint32_t)pool_grid_of(d_) * (kBlock / 64);
   PoolTable& t = *d_.h_tab[ring_];
   uint32_t n = 0;
   bool bounded = false;
@@ -298,6 +330,8 @@ int Worker::launch() {
   t.n = n;
   t.poll_mask = poll_mask();
   t.iters = iters;
+  t.budget = g_budget_us.load() * 100u;  // s_memrealtime runs at 100 MHz
+  t.yield_base = __atomic_load_n(&d_.pmb->yield, __ATOMIC_ACQUIRE);
   ++seq_;
   {
     std::lock_guard<std::mutex> g(g_pool.mu);  // issued[] is shared with other workers' reads
@@ -322,6 +356,7 @@ int Worker::launch() {
       }
       issued += pe.count;
       if (j.max_per_dev && issued >= j.max_per_dev) sl.no_more = true;
+      sl.fresh = false;
     }
   }
   const int r = ring_;
@@ -332,8 +367,9 @@ int Worker::launch() {
   // the copy is a blit kernel that competes with the running launch.)
   HIPTRY(hipMemcpyAsync(d_.d_tab[r], d_.h_tab[r], bytes, hipMemcpyHostToDevice, d_.stream));
   HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
-  HIPTRY(launch_pool(grid_of(d_), d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
+  HIPTRY(launch_pool(pool_grid_of(d_), d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
   HIPTRY(hipEventRecord(d_.ev_stop[r], d_.stream));
+  if (q_.empty()) front_start_ = std::chrono::steady_clock::now();
   q_.push_back({seq_, r});
   return NPOW_OK;
 }
@@ -360,6 +396,7 @@ int Worker::retire() {
     if (e != hipSuccess) return fail(NPOW_ERR_HIP, std::string("pool launch: ") + hipGetErrorString(e));
     account_launch(d_, q_.front().ring);
     q_.pop_front();
+    front_start_ = std::chrono::steady_clock::now();  // the next one (if any) has just started
   }
   constexpr size_t row = kPoolDoneShards * 8;
   for (int s = 0; s < kMaxSlots; ++s) {

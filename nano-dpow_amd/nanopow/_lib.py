@@ -37,6 +37,7 @@ EXPORTED_SYMBOLS = (
     "npow_search_batch", "npow_sweep", "npow_values", "npow_values_pairs", "npow_set_tuning",
     "npow_device_stats_get", "npow_device_stats_reset", "npow_version",
     "npow_submit", "npow_wait", "npow_cancel", "npow_pool_config", "npow_pool_status",
+    "npow_set_pool_tuning",
 )
 
 
@@ -121,6 +122,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.npow_pool_config.restype = ctypes.c_int
         lib.npow_pool_status.argtypes = [ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32)]
         lib.npow_pool_status.restype = ctypes.c_int
+        lib.npow_set_pool_tuning.argtypes = [u32, u32]
+        lib.npow_set_pool_tuning.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -288,6 +291,14 @@ class Engine:
 
     def set_tuning(self, iters_per_launch: int = 0, poll_interval: int = 0, blocks_per_cu: int = 0) -> None:
         _check(self.lib.npow_set_tuning(iters_per_launch, poll_interval, blocks_per_cu), self.lib)
+
+    def set_pool_tuning(self, budget_us: Optional[int] = None, blocks_per_cu: int = 0) -> None:
+        """Search launches: time budget in us (0 = off, None keeps) and workgroups per CU (0 keeps)."""
+        _check(self.lib.npow_set_pool_tuning(0xffffffff if budget_us is None else budget_us, blocks_per_cu),
+               self.lib)
+
+    def set_launch_budget(self, budget_us: int) -> None:
+        self.set_pool_tuning(budget_us=budget_us)
 
     def stats(self, device: int = 0) -> DeviceStats:
         s = DeviceStats()

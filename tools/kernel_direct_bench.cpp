@@ -5,12 +5,13 @@
 //   pool8 = npow_pool_kernel<false> with eight unbounded entries
 // Build: hipcc -O3 --offload-arch=gfx950 -Inano-dpow_amd/csrc -Iinclude -x hip tools/kernel_direct_bench.cpp
 //        -x none nano-dpow_amd/csrc/npow_kernel.o -o build/kernel_direct_bench
-// Run:   ./build/kernel_direct_bench [reps] [iters] [poll_mask]
+// Run:   ./build/kernel_direct_bench [reps] [iters] [poll_mask] [gap_us] [blocks_per_cu]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <unistd.h>
 #include <vector>
 
 #include "npow_internal.h"
@@ -30,10 +31,12 @@ int main(int argc, char** argv) {
   const int reps = argc > 1 ? atoi(argv[1]) : 20;
   const uint32_t iters = argc > 2 ? (uint32_t)atoi(argv[2]) : 256;
   const uint32_t pmask = argc > 3 ? (uint32_t)atoi(argv[3]) : 1023;  // host-word poll mask
+  const int gap_us = argc > 4 ? atoi(argv[4]) : 0;                      // host sleep between launches
+  const int bpc = argc > 5 ? atoi(argv[5]) : 8;                          // workgroups per CU
   CK(hipSetDevice(0));
   hipDeviceProp_t p;
   CK(hipGetDeviceProperties(&p, 0));
-  const int grid = p.multiProcessorCount * 8;
+  const int grid = p.multiProcessorCount * bpc;
   const uint64_t W = (uint64_t)grid * (kBlock / 64);
   hipStream_t s;
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -97,6 +100,7 @@ int main(int argc, char** argv) {
       }
       CK(hipEventRecord(e1, s));
       CK(hipEventSynchronize(e1));
+      if (gap_us > 0) usleep(gap_us);
       float ms = 0;
       CK(hipEventElapsedTime(&ms, e0, e1));
       if (r > 0) tot[v] += ms;
