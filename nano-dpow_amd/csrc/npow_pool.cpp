@@ -25,6 +25,7 @@
 #include <chrono>
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <memory>
@@ -41,6 +42,11 @@ namespace {
 
 constexpr int kPending = 100;  // job status before it is decided
 constexpr double kYieldMinUs = 1500.0;  // yield a running launch only if more budget than this is left
+const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
+#define NPOW_DBG(...)                     \
+  do {                                    \
+    if (g_debug) fprintf(stderr, __VA_ARGS__); \
+  } while (0)
 
 struct Job {
   uint64_t ticket = 0;
@@ -52,6 +58,7 @@ struct Job {
   // guarded by g_pool.mu
   std::vector<uint64_t> issued;     // per device k: nonces of its stride handed to launches
   std::vector<uint8_t> on_dev;      // per device k: a slot holds the job
+  std::vector<uint8_t> seen_dev;    // per device k: adopted at least once (re-adoptions do not yield)
   std::vector<uint8_t> dev_done;    // per device k: finished with the job
   std::vector<int> invalid_streak;  // per device k
   int pending_devs = 0;
@@ -230,7 +237,8 @@ void Worker::adopt() {
     sl.win_seen = sl.requeue = sl.no_more = sl.readback = false;
     sl.fresh = true;
     j->on_dev[k] = 1;
-    adopted = true;
+    if (!j->seen_dev[k]) adopted = true;  // a new job: worth ending a long launch for
+    j->seen_dev[k] = 1;
   }
   if (adopted) yield_if_long();
 }
@@ -244,6 +252,7 @@ void Worker::yield_if_long() {
   if (q_.empty() || g_budget_us.load() == 0) return;
   const double left_us = g_budget_us.load() - std::chrono::duration<double, std::micro>(
                                                   std::chrono::steady_clock::now() - front_start_).count();
+  NPOW_DBG("nanopow[%d]: yield? inflight %zu left_us %.0f\n", d_.id, q_.size(), left_us);
   if (q_.size() < 2 && left_us < kYieldMinUs) return;
   bool any = false;
   for (Slot& sl : slots_) {
@@ -252,6 +261,7 @@ void Worker::yield_if_long() {
     sl.state = SlotState::kDraining;
     any = true;
   }
+  NPOW_DBG("nanopow[%d]: yield %s\n", d_.id, any ? "raised" : "(no slot to hand back)");
   if (any) {
     __atomic_store_n(&d_.pmb->yield, __atomic_load_n(&d_.pmb->yield, __ATOMIC_RELAXED) + 1, __ATOMIC_RELEASE);
     ++yields_;
@@ -370,6 +380,9 @@ int Worker::launch() {
   HIPTRY(launch_pool(pool_grid_of(d_), d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
   HIPTRY(hipEventRecord(d_.ev_stop[r], d_.stream));
   if (q_.empty()) front_start_ = std::chrono::steady_clock::now();
+  NPOW_DBG("nanopow[%d]: launch %llu n=%u slots:", d_.id, (unsigned long long)seq_, n);
+  for (uint32_t e = 0; e < n; ++e) NPOW_DBG(" %d/g%llu", idx[e], (unsigned long long)t.e[e].gen);
+  NPOW_DBG("\n");
   q_.push_back({seq_, r});
   return NPOW_OK;
 }
@@ -395,6 +408,7 @@ int Worker::retire() {
     if (e == hipErrorNotReady) break;
     if (e != hipSuccess) return fail(NPOW_ERR_HIP, std::string("pool launch: ") + hipGetErrorString(e));
     account_launch(d_, q_.front().ring);
+    NPOW_DBG("nanopow[%d]: launch %llu done\n", d_.id, (unsigned long long)q_.front().seq);
     q_.pop_front();
     front_start_ = std::chrono::steady_clock::now();  // the next one (if any) has just started
   }
@@ -415,6 +429,8 @@ int Worker::retire() {
       d_.nonces += delta;
     }
     if (win_published(s)) handle_win(s);  // published by the last launch, not yet seen
+    NPOW_DBG("nanopow[%d]: retire slot %d g%llu done %llu requeue %d\n", d_.id, s, (unsigned long long)sl.gen,
+             (unsigned long long)delta, (int)sl.requeue);
     {
       std::lock_guard<std::mutex> g(g_pool.mu);
       Job& j = *sl.job;
@@ -589,6 +605,7 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   for (Device* d : devs) j->devs.push_back(d->id);
   j->issued.assign(G, 0);
   j->on_dev.assign(G, 0);
+  j->seen_dev.assign(G, 0);
   j->dev_done.assign(G, 0);
   j->invalid_streak.assign(G, 0);
   j->pending_devs = (int)G;

@@ -192,3 +192,27 @@ def test_full_table_of_64_bounded_and_unbounded(gpu_engine):
     for root, t in zip(roots[32:], ut):
         r = t.wait(60)
         assert r.status == _lib.NPOW_OK and oracle.work_value(root, r.nonce) == r.value >= LOW
+
+
+def test_new_job_does_not_wait_for_a_long_launch(gpu_engine):
+    """With a 200-ms launch budget, a job submitted while another job's launch is running is
+    searched within a few ms: the worker bumps the yield word, the running launch hands its
+    unbounded job back (re-adopted with a new generation), and the next launch holds both."""
+    gpu_engine.set_pool_tuning(budget_us=200_000)
+    try:
+        tok = _lib.CancelToken()
+        busy = gpu_engine.submit(bytes(range(32)), M64, device_mask=1, cancel=tok)
+        time.sleep(0.05)  # the busy job's first 200-ms launch is running
+        lat = []
+        for r in _roots(18, 5):
+            t0 = time.perf_counter()
+            res = gpu_engine.submit(r, RECEIVE, device_mask=1).wait(10)
+            lat.append(time.perf_counter() - t0)
+            assert res.status == _lib.NPOW_OK and oracle.work_value(r, res.nonce) == res.value >= RECEIVE
+        assert max(lat) < 0.1, lat
+        assert busy.wait(0) is None  # still searching after being handed back
+        tok.set()
+        res = busy.wait(10)
+        assert res.status == _lib.NPOW_CANCELLED and res.nonces_done > 0
+    finally:
+        gpu_engine.set_pool_tuning(budget_us=20_000)
