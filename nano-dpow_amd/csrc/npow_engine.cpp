@@ -45,7 +45,9 @@ const std::string& last_error() { return t_err; }
 std::vector<std::unique_ptr<Device>> g_devs;
 std::atomic<uint32_t> g_iters{8192};    // search launches: iteration cap under the time budget (the oldest wave of a
                                         // SIMD runs ~4 us per iteration, ~5,000 in 20 ms) and the span of bounded jobs
-constexpr uint32_t kSweepIters = 512;   // sweep launches: wave iterations (2^28 nonces, ~10 ms)
+constexpr uint32_t kSweepIters = 4096;  // sweep launches: mean wave iterations (2^31 nonces, ~80 ms; a launch
+                                        // costs ~0.35 ms of ramp-up and drain: 26.46 Gnonce/s at 20 ms, 26.93 at 80 ms)
+constexpr uint32_t kSweepMaxClaim = 64;  // sweep: most wave iterations per claim (npow_task_kernel)
 std::atomic<uint32_t> g_poll{1024};     // a wave reads the host word every g_poll iterations (8 waves per iteration grid-wide)
 std::atomic<uint32_t> g_blocks_per_cu{8};
 std::atomic<uint32_t> g_budget_us{20000};  // pool launches end on time, not on their slowest wave
@@ -149,8 +151,10 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
   a.threshold = threshold;
   a.poll_mask = poll_mask();
   a.cap = (uint32_t)kHitCap;
+  a.max_claim = kSweepMaxClaim;
   const uint64_t chunk = (uint64_t)grid_of(d) * kBlock * kSweepIters;
   uint64_t issued = 0;
+  uint32_t launches = 0;  // parity picks the launch's claim counter (reset_task zeroed both)
   int ring = 0;
   std::deque<Inflight> q;
   cancelled = false;
@@ -159,6 +163,7 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
       const uint64_t cnt = std::min(chunk, count - issued);
       a.base = start + issued;
       a.count = cnt;
+      a.claim_slot = launches++ & 1;
       rc = launch_chunk(d, Mode::kSweep, a, ring, d.d_out);
       if (rc) return rc;
       q.push_back({ring, cnt});

@@ -23,6 +23,8 @@ struct LaunchArgs {
   uint64_t count;      // nonces in this launch (lane index i < count)
   uint32_t poll_mask;  // a wave polls the host abort word when (iter & poll_mask) == 0
   uint32_t cap;        // sweep: capacity of the hit buffer
+  uint32_t claim_slot; // sweep: DevState::claim[claim_slot] is this launch's work counter
+  uint32_t max_claim;  // sweep: most 64-nonce wave iterations one claim takes
 };
 
 // Device-resident per-task state (hipMalloc; reset by hipMemsetAsync per task).
@@ -44,6 +46,11 @@ struct DevState {
   uint64_t value;           // winning value (search)
   uint32_t zero;            // always 0: the non-polling iterations' load target
   uint8_t pad1[64 - 36];
+  // Sweep work counters (64-nonce wave iterations claimed so far), one per launch parity:
+  // launch k claims from claim[k & 1] and zeroes claim[(k + 1) & 1] for launch k + 1 (same
+  // stream, so launch k - 1, its previous user, has finished).  Own cache lines: every wave
+  // polls `stop` above each iteration.
+  unsigned long long claim[2 * 8];
   unsigned long long done_shard[kDoneShards * 8];  // nonces hashed, one counter per 64-byte line
   uint64_t done() const {
     uint64_t s = 0;

@@ -121,34 +121,27 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
   // First lane index of this wave; wave-uniform.
   const uint64_t wave0 =
       (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kBlock + (threadIdx.x & ~63u));
-  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
   const uint32_t wave_id = (uint32_t)(wave0 >> 6);
   uint64_t done = 0;  // nonces this wave hashed (wave-uniform)
   uint32_t iter = 0;
 
-  for (uint64_t ib = wave0; ib < a.count; ib += stride, ++iter) {
+  // One 64-nonce wave iteration at lane offset ib; false = stop (abort / stop word).
+  auto step = [&](uint64_t ib) -> bool {
     // Early-exit polls:
     //  * every iteration, one agent-scope (L2) load of the device stop word
-    //    {found, abort} -- set by a winning wave or relayed from the host; it is
-    //    issued first and consumed after the hash, so its latency is hidden;
-    //  * the host abort word lives in pinned host memory (a PCIe read whose
-    //    latency and throughput vary by host: on some boxes thousands of
-    //    concurrent reads queue up for tens of microseconds), so only one wave in
-    //    poll_mask+1 reads it per iteration (staggered by wave id: with the
-    //    default 1024 that is 8 waves per iteration grid-wide) and relays a raised
-    //    abort into the device stop word.
+    //    {found, abort} -- relayed from the host; it is issued first and consumed after
+    //    the hash, so its latency is hidden;
+    //  * the host abort word lives in pinned host memory (a PCIe read whose latency and
+    //    throughput vary by host), so only one wave in poll_mask+1 reads it per iteration
+    //    (staggered by wave id) and relays a raised abort into the device stop word.
     uint64_t stop_word = 0;
     uint32_t host_abort = 0;
-#ifndef NPOW_POLL_MODE
-#define NPOW_POLL_MODE 2
-#endif
     if constexpr (MODE != Mode::kValues) {
-      if (NPOW_POLL_MODE >= 1)
-        stop_word = __hip_atomic_load(&st->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (NPOW_POLL_MODE >= 2 && ((iter + wave_id) & a.poll_mask) == 0)
+      stop_word = __hip_atomic_load(&st->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (((iter + wave_id) & a.poll_mask) == 0)
         host_abort = __hip_atomic_load(&mb->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
-
+    ++iter;
     const uint64_t i = ib + lane;
     const uint64_t nonce = a.base + i;
     const uint64_t value = npow_asm_work_value(nonce, u);
@@ -167,9 +160,43 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
       }
       if (__builtin_amdgcn_readfirstlane(host_abort)) {
         if (lane == 0) __hip_atomic_store(&st->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
+        return false;
       }
-      if (__builtin_amdgcn_readfirstlane((uint32_t)stop_word | (uint32_t)(stop_word >> 32))) break;
+      if (__builtin_amdgcn_readfirstlane((uint32_t)stop_word | (uint32_t)(stop_word >> 32))) return false;
+    }
+    return true;
+  };
+
+  if constexpr (MODE == Mode::kValues) {
+    // Static grid-stride mapping (parity tests: no hits, no early exit).
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    for (uint64_t ib = wave0; ib < a.count; ib += stride) step(ib);
+  } else {
+    // Sweep: waves claim runs of 64-nonce iterations from the launch's counter (guided
+    // self-scheduling: a claim takes remaining / (2 W) iterations, at least 1, at most
+    // max_claim).  VALU issue favours a SIMD's oldest wave, so with a fixed per-wave share
+    // the young waves finish late and the launch ends in a tail with one or two waves per
+    // SIMD; claiming keeps every SIMD full until the range is used up.
+    unsigned long long* ctr = &st->claim[(a.claim_slot & 1) * 8];
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      __hip_atomic_store(&st->claim[((a.claim_slot + 1) & 1) * 8], 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t T = (a.count + 63) >> 6;                    // wave iterations in the launch
+    const uint64_t W2 = 2ull * gridDim.x * (kBlock / 64);      // 2 x waves in the launch
+    uint64_t seen = 0;                                         // counter value at the last claim
+    for (;;) {
+      const uint64_t left = T > seen ? T - seen : 0;
+      uint64_t n = left / W2;
+      n = n < 1 ? 1 : (n > a.max_claim ? a.max_claim : n);
+      uint64_t c = 0;
+      if (lane == 0) c = atomicAdd(ctr, (unsigned long long)n);
+      c = readlane64(c, 0);
+      if (c >= T) break;
+      seen = c + n;
+      const uint64_t end = seen < T ? seen : T;
+      bool go = true;
+      for (uint64_t k = c; k < end && go; ++k) go = step(k << 6);
+      if (!go) break;
     }
   }
   if (lane == 0 && done) atomicAdd(&st->done_shard[(blockIdx.x % kDoneShards) * 8], (unsigned long long)done);

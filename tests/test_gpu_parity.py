@@ -71,6 +71,28 @@ def test_sweep_2p36_full_size(gpu_engine):
     print(f"2^36 sweep: {len(got)} hits in {dt:.2f} s = {(1 << 36) / dt / 1e9:.2f} Gnonce/s")
 
 
+def test_sweep_ragged_multi_launch_subranges(gpu_engine):
+    """Sweep launches claim 64-nonce runs from a counter that alternates between two cache
+    lines by launch parity: ragged sub-ranges of the 2^36 fixture spanning 1-3 launches
+    (2^31 nonces each) return exactly the fixture's hits inside them."""
+    g = load_golden("sweep_2p36.json")
+    root, thr = bytes.fromhex(g["root"]), int(g["threshold"], 16)
+    hits = [int(h, 16) for h in g["hits"]]
+    for lo, n in [(12345, (1 << 31) + 77), (5 << 33, (3 << 31) - 1), (hits[3] - 1, 2)]:
+        want = [h for h in hits if lo <= h < lo + n]
+        assert gpu_engine.sweep(root, thr, lo, n, cap=1 << 12) == want, (lo, n)
+
+
+def test_sweep_every_nonce_a_hit_exactly_once(gpu_engine):
+    """Threshold 0 makes every nonce a hit: the claim counter covers each nonce exactly once,
+    also for a count that is not a multiple of 64 or of the claim size (one launch; the
+    device hit buffer holds 2^20)."""
+    root = bytes(range(5, 37))
+    n = 1_000_003
+    got = gpu_engine.sweep(root, 0, 1 << 50, n, cap=n)
+    assert got == [(1 << 50) + i for i in range(n)]
+
+
 def test_sweep_edges(gpu_engine):
     root = bytes(range(32))
     assert gpu_engine.sweep(root, 0, 5, 0) == []

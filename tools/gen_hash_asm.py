@@ -261,7 +261,11 @@ def lower(dag: Dag, out: Node):
 
 # issue cost (SIMD cycles per wave64 instruction, profiles/r01_valu_ubench.json) and latency model
 COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b32": 4.3, "v_lshl_add_u64": 4.4,
-        "v_lshrrev_b32": 2.5, "v_mov_b32": 2.4}
+        "v_lshrrev_b32": 2.5, "v_mov_b32": 2.4, "v_add_co_u32": 2.1, "v_addc_co_u32": 2.1}
+# 64-bit add as v_add_co_u32 + v_addc_co_u32 (carry through VCC) instead of one v_lshl_add_u64:
+# both issue at full rate next to xors (profiles/r01_valu_mix2.jsonl), v_lshl_add_u64 does not
+ADD_CC = False
+ROTL1_CC = False  # rotr63 = x + x + carry as v_add_co_u32 + 2x v_addc_co_u32
 ROTL1_VIA_ADD = True  # rotr63 = (x << 1) + (x >> 63): v_lshrrev_b32 + v_lshl_add_u64 with a zero partner
 # Measured on MI355X (tools/valu_patterns.py): in a stream that mixes in 64-bit / 3-operand VALU
 # ops, VOP2-encoded v_xor_b32 issues at ~4.1 SIMD cycles but its VOP3 (_e64) encoding at ~2.6.
@@ -370,7 +374,7 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
     # {t, 0} pairs for rotr63 = (x << 1) + (x >> 63): the odd register of each holds zero
     zpairs = []
     lines_pre: List[str] = []
-    if ROTL1_VIA_ADD:
+    if ROTL1_VIA_ADD and not ROTL1_CC:
         for _ in range(2):
             r = al.take2()
             zpairs.append(r)
@@ -442,11 +446,26 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             ta, tb = pair(a), pair(b)
             if a.uniform:  # VOP3 src0 may be an SGPR pair too, keep the VGPR first for readability
                 ta, tb = tb, ta
+            # VOP2 co/addc: src1 must be a VGPR, src0 may be an SGPR; v{r} (even) never aliases a hi half
+            x, y = (b, a) if a.uniform else (a, b)
+            if y.uniform:
+                x, y = y, x
+            # v_addc reads VCC over the constant bus, which gfx950 allows only one read per
+            # instruction: an add with an SGPR/literal operand stays one v_lshl_add_u64
+            cc = ADD_CC and not (a.uniform or b.uniform)
+            hx = [half(x, 0), half(x, 1)] if cc else None
+            hy = [half(y, 0), half(y, 1)] if cc else None
             consume(op)
             r = al.take2()
             loc[op.dst.id] = r
-            lines.append(f"v_lshl_add_u64 v[{r}:{r + 1}], {ta}, 0, {tb}")
-            cnt("v_lshl_add_u64")
+            if cc:
+                lines.append(f"v_add_co_u32 v{r}, vcc, {hx[0]}, {hy[0]}")
+                lines.append(f"v_addc_co_u32 v{r + 1}, vcc, {hx[1]}, {hy[1]}, vcc")
+                cnt("v_add_co_u32")
+                cnt("v_addc_co_u32")
+            else:
+                lines.append(f"v_lshl_add_u64 v[{r}:{r + 1}], {ta}, 0, {tb}")
+                cnt("v_lshl_add_u64")
         elif op.kind == "xrot32" and SWAP_MOV:
             s0h, s1h = xor_operands(a, b, 1)
             s0l, s1l = xor_operands(a, b, 0)
@@ -478,6 +497,24 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             lines.append(f"v_xor_b32 v{r + 1}, {s0l}, {s1l}")
             cnt("v_xor_b32")
             cnt("v_xor_b32")
+        elif op.kind == "xrot" and op.n == 63 and ROTL1_CC:
+            # rotl1(x) = x + x + (x >> 63): lo+lo carries lo's top bit into hi+hi, whose own carry-out
+            # (hi's top bit) is added back into the (even) low word
+            s0l, s1l = xor_operands(a, b, 0)
+            s0h, s1h = xor_operands(a, b, 1)
+            consume(op)
+            r = al.take2()
+            lines.append(f"v_xor_b32 v{r}, {s0l}, {s1l}")
+            lines.append(f"v_xor_b32 v{r + 1}, {s0h}, {s1h}")
+            lines.append(f"v_add_co_u32 v{r}, vcc, v{r}, v{r}")
+            lines.append(f"v_addc_co_u32 v{r + 1}, vcc, v{r + 1}, v{r + 1}, vcc")
+            lines.append(f"v_addc_co_u32 v{r}, vcc, 0, v{r}, vcc")
+            loc[op.dst.id] = r
+            cnt("v_xor_b32")
+            cnt("v_xor_b32")
+            cnt("v_add_co_u32")
+            cnt("v_addc_co_u32")
+            cnt("v_addc_co_u32")
         elif op.kind == "xrot" and op.n == 63 and ROTL1_VIA_ADD:
             s0l, s1l = xor_operands(a, b, 0)
             s0h, s1h = xor_operands(a, b, 1)
@@ -821,6 +858,7 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
         else:
             regs[int(tok[1:])] = val & M32
 
+    vcc = 0
     for ln in lines:
         if ln.startswith(".") or ln.startswith("s_nop"):
             continue  # placement directives / padding
@@ -836,6 +874,16 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
             wr32(ops[0], rd32(ops[2]) >> int(ops[1]))
         elif opc == "v_mov_b32":
             wr32(ops[0], rd32(ops[1]))
+        elif opc == "v_add_co_u32":
+            assert ops[1] == "vcc"
+            t = rd32(ops[2]) + rd32(ops[3])
+            wr32(ops[0], t)
+            vcc = t >> 32
+        elif opc == "v_addc_co_u32":
+            assert ops[1] == "vcc" and ops[4] == "vcc"
+            t = rd32(ops[2]) + rd32(ops[3]) + vcc
+            wr32(ops[0], t)
+            vcc = t >> 32
         elif opc == "v_lshl_add_u64":
             x = (rd64(ops[1]) << int(ops[2])) & M64
             y = rd64(ops[3])
@@ -901,6 +949,8 @@ def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List
     nu = len(frontier)
     clobbers = ", ".join(f'"v{r}"' for r in range(vbase, vmax))
     text = "\n".join(lines)
+    if "vcc" in text:
+        clobbers += ', "vcc"'
     ops_in = []
     for nm, expr in [("nonce", "nonce"), ("nonce_lo", "(uint32_t)nonce"), ("nonce_hi", "(uint32_t)(nonce >> 32)")]:
         if f"%[{nm}]" in text:
@@ -961,18 +1011,23 @@ def main() -> int:
     ap.add_argument("--out", default=os.path.join(os.path.dirname(os.path.abspath(__file__)), "..",
                                                   "nano-dpow_amd", "csrc", "npow_hash_asm.inc"))
     ap.add_argument("--check", type=int, default=64, help="random (root, nonce) pairs to check vs hashlib")
-    ap.add_argument("--rotl1", choices=["add", "alignbit"], default="add",
-                    help="rotr63 as v_lshrrev_b32 + v_lshl_add_u64 (add) or two v_alignbit_b32")
+    ap.add_argument("--rotl1", choices=["add", "alignbit", "cc"], default="add",
+                    help="rotr63 as v_lshrrev_b32 + v_lshl_add_u64 (add), two v_alignbit_b32, or a "
+                         "v_add_co_u32 + 2x v_addc_co_u32 carry chain (cc)")
+    ap.add_argument("--add", choices=["u64", "cc"], default="u64",
+                    help="64-bit add as one v_lshl_add_u64 (u64) or v_add_co_u32 + v_addc_co_u32 (cc)")
     ap.add_argument("--enc", choices=["vop3", "vop2"], default="vop3",
                     help="encoding of the simple 32-bit ops (xor, lshrrev)")
     ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
     ap.add_argument("--pad", choices=["odd", "even", "none"], default="odd",
                     help="placement of the stream: 4 (mod 8) [odd], 0 (mod 8) [even], or as it falls")
     args = ap.parse_args()
-    global ROTL1_VIA_ADD, VOP3_SIMPLE, SWAP_MOV, PAD
+    global ROTL1_VIA_ADD, VOP3_SIMPLE, SWAP_MOV, PAD, ADD_CC, ROTL1_CC
+    ADD_CC = args.add == "cc"
     SWAP_MOV = args.swapmov
     PAD = {"odd": ['.p2align 3', 's_nop 0'], "even": ['.p2align 3'], "none": []}[args.pad]
     ROTL1_VIA_ADD = args.rotl1 == "add"
+    ROTL1_CC = args.rotl1 == "cc"
     VOP3_SIMPLE = args.enc == "vop3"
 
     dag, out = build_hash_dag()
@@ -1007,7 +1062,7 @@ def main() -> int:
             print(f"MISMATCH root={root.hex()} nonce={nonce:016x} got={got:016x} want={want:016x}")
             return 1
     host_prog = c_expr_program(frontier)
-    write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --enc {args.enc}" + (" --swapmov" if args.swapmov else "")
+    write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --add {args.add} --enc {args.enc}" + (" --swapmov" if args.swapmov else "")
               + (f" --lat {args.lat:g} --window {args.window}" if args.sched == "ilp" else "") + f" --pad {args.pad}", est)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
           f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")

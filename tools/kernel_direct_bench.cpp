@@ -65,6 +65,7 @@ int main(int argc, char** argv) {
   a.threshold = ~0ull;
   a.poll_mask = pmask;
   a.count = W * 64 * iters;
+  a.max_claim = 64;
 
   PoolTable* tabs[2];
   for (int k = 0; k < 2; ++k) {
@@ -94,6 +95,7 @@ int main(int argc, char** argv) {
     for (int v = 0; v < 3; ++v) {
       CK(hipEventRecord(e0, s));
       if (v == 0) {
+        a.claim_slot = (uint32_t)r & 1;
         CK(launch_task(Mode::kSweep, grid, s, a, st, mbd, nullptr));
       } else {
         CK(launch_pool(grid, s, tabs[v - 1], false, pst, pmbd));
