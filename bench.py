@@ -474,6 +474,32 @@ def _hashlib_search(root: bytes, thr: int, start: int, limit: int):
     return limit, None
 
 
+def _http_ttw(eng, n):
+    """BASELINE config 2 at the JSON boundary: n work_generate requests at fffffff8 POSTed one
+    at a time to the HTTP work server on 127.0.0.1 (fresh roots past the timed ones); wall
+    time per POST -> reply, each reply re-validated through npow_work_value."""
+    from nanopow.server import HttpWorkServer, WorkServer
+    import urllib.request
+    srv = HttpWorkServer(WorkServer(eng, max_active=1, device_mask=1), "127.0.0.1", 0).start()
+    out = []
+    try:
+        for i in range(n):
+            root = bench_root(30_000_000 + i)
+            body = json.dumps({"action": "work_generate", "hash": root.hex().upper(),
+                               "difficulty": f"{SEND:016x}"}).encode()
+            t = time.perf_counter()
+            req = urllib.request.Request(f"http://{srv.address}", data=body, method="POST",
+                                         headers={"Content-Type": "application/json"})
+            with urllib.request.urlopen(req, timeout=60) as resp:
+                rep = json.loads(resp.read())
+            out.append(time.perf_counter() - t)
+            if eng.work_value(root, int(rep["work"], 16)) < SEND:
+                raise RuntimeError(f"HTTP reply {rep} does not validate")
+    finally:
+        srv.stop()
+    return out
+
+
 def workload_receive(eng, args, rank, world, dist):
     """BASELINE config 1: work_generate at fffffe0000000000, GPU next to the CPU reference."""
     if world > 1:
@@ -558,6 +584,8 @@ def main() -> int:
     ap.add_argument("--rate", type=float, default=20.0, help="dpow: work messages per second")
     ap.add_argument("--concurrency", type=int, default=1, help="dpow: WorkHandler loops (reference: 1)")
     ap.add_argument("--cpu-requests", type=int, default=4, help="receive: requests timed on the CPU reference")
+    ap.add_argument("--http-requests", type=int, default=100,
+                    help="search, N=1: work_generate requests timed at the JSON boundary after the timed steps")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -598,8 +626,13 @@ def main() -> int:
         return st.kernel_ms, st.nonces, st.launches
 
     res = run_timed(search, stats, lambda: eng.reset_stats(dev), args.steps, args.warmup, rank, WORLD, dist)
+    http = _http_ttw(eng, args.http_requests) if (rank == 0 and WORLD == 1 and args.http_requests) else None
     if rank == 0:
         line = result_line(WORLD, args.steps, args.warmup, *res)
+        if http:
+            line["http_ttw_ms"] = {"p50": round(pct(http, 50) * 1e3, 3), "p99": round(pct(http, 99) * 1e3, 3),
+                                   "n": len(http), "note": "POST work_generate -> reply at the JSON boundary "
+                                   "(127.0.0.1 HTTP work server), after the timed region; not part of value"}
         if WORLD == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = cpu_baseline()
         print(json.dumps(line), flush=True)
