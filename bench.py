@@ -148,12 +148,13 @@ def run_timed(search, stats, reset_stats, steps: int, warmup: int, rank: int, wo
     return int(v[0]), float(w_t[0]), all_ttw, float(v[1]), int(v[2]), int(v[3])
 
 
-def _pmc_traffic():
-    """HBM bytes per npow_pool_kernel launch measured by rocprofv3 PMC passes (tools/pmc_pool.sh on
-    this bench's workload; FETCH_SIZE doubled per the gfx950 correction).  PMC needs the profiler
-    around the process, so the bench reports the committed measurement; None if absent."""
+def _pmc_traffic(name="r01_pmc_pool.json"):
+    """HBM bytes per launch of the workload's dominant kernel measured by rocprofv3 PMC passes
+    (tools/pmc_bench.sh on that workload; FETCH_SIZE doubled per the gfx950 correction).  PMC
+    needs the profiler around the process, so the bench reports the committed measurement;
+    None if absent."""
     try:
-        with open(os.path.join(HERE, "profiles", "r01_pmc_pool.json")) as f:
+        with open(os.path.join(HERE, "profiles", name)) as f:
             return json.load(f)["hbm_bytes_per_launch"]
     except (OSError, ValueError, KeyError):
         return None
@@ -196,7 +197,7 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
             "frac": round(achieved / PEAK_TOPS, 4),
             "traffic": _pmc_traffic(),
             "traffic_unit": "HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
-                            "(profiles/r01_pmc_pool.json, tools/pmc_pool.sh); algorithmic bytes: 0",
+                            "(profiles/r01_pmc_pool.json, tools/pmc_bench.sh); algorithmic bytes: 0",
             "ops_per_nonce": OPS_PER_NONCE,
             "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
             "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
@@ -278,6 +279,10 @@ def workload_sweep(eng, args, rank, world, dist):
     want = [int(h, 16) for h in fx["hits"] if int(h, 16) < count]
     line = result_line(world, 1, 0, nonces, wall, [wall], kms, kn, nl)
     line["roofline"]["kernel"] = "npow_task_kernel<Mode::kSweep>"
+    line["roofline"]["traffic"] = _pmc_traffic("r01_pmc_sweep.json")
+    line["roofline"]["traffic_unit"] = ("HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
+                                        "(profiles/r01_pmc_sweep.json, tools/pmc_bench.sh); algorithmic bytes: "
+                                        "8 per hit")
     line["config"] = {"workload": f"BASELINE configs[2]: exhaustive sweep of [0, 2^{args.sweep_bits}) for the "
                                   "fixture root at fffffff800000000, ranks split the range",
                       "threshold": fx["threshold"], "count": count,

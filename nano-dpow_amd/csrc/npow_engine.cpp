@@ -47,7 +47,19 @@ std::atomic<uint32_t> g_iters{8192};    // search launches: iteration cap under 
                                         // SIMD runs ~4 us per iteration, ~5,000 in 20 ms) and the span of bounded jobs
 constexpr uint32_t kSweepIters = 4096;  // sweep launches: mean wave iterations (2^31 nonces, ~80 ms; a launch
                                         // costs ~0.35 ms of ramp-up and drain: 26.46 Gnonce/s at 20 ms, 26.93 at 80 ms)
-constexpr uint32_t kSweepMaxClaim = 64;  // sweep: most wave iterations per claim (npow_task_kernel)
+// Sweep: most wave iterations per claim (npow_task_kernel).  Plain guided self-scheduling
+// (first claims T / 2W, ~2,048 iterations) assumes equally fast workers; here a SIMD's
+// youngest wave runs several times slower than its oldest, and a young wave still holding a
+// 2,048-iteration claim becomes the launch's tail (25.81 Gnonce/s vs 26.89 at 64).
+// NANOPOW_SWEEP_CLAIM overrides (experiments).
+uint32_t sweep_max_claim() {
+  static const uint32_t v = [] {
+    const char* e = getenv("NANOPOW_SWEEP_CLAIM");
+    const int k = e ? atoi(e) : 0;
+    return k > 0 ? (uint32_t)k : 64u;
+  }();
+  return v;
+}
 std::atomic<uint32_t> g_poll{1024};     // a wave reads the host word every g_poll iterations (8 waves per iteration grid-wide)
 std::atomic<uint32_t> g_blocks_per_cu{8};
 std::atomic<uint32_t> g_budget_us{20000};  // pool launches end on time, not on their slowest wave
@@ -151,7 +163,7 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
   a.threshold = threshold;
   a.poll_mask = poll_mask();
   a.cap = (uint32_t)kHitCap;
-  a.max_claim = kSweepMaxClaim;
+  a.max_claim = sweep_max_claim();
   const uint64_t chunk = (uint64_t)grid_of(d) * kBlock * kSweepIters;
   uint64_t issued = 0;
   uint32_t launches = 0;  // parity picks the launch's claim counter (reset_task zeroed both)

@@ -32,6 +32,7 @@ struct LaunchArgs {
 // count once at exit, and 8,192 waves adding to ONE word serialise at the memory
 // side (~12 ns each, MI355X_MICROARCH.md "fanin") -- a ~100 us tail on every launch.
 constexpr int kDoneShards = 256;
+constexpr int kClaimRanges = 8;  // sweep sub-ranges per launch (one per XCD), npow_task_kernel
 struct DevState {
   union {
     struct {
@@ -46,11 +47,12 @@ struct DevState {
   uint64_t value;           // winning value (search)
   uint32_t zero;            // always 0: the non-polling iterations' load target
   uint8_t pad1[64 - 36];
-  // Sweep work counters (64-nonce wave iterations claimed so far), one per launch parity:
-  // launch k claims from claim[k & 1] and zeroes claim[(k + 1) & 1] for launch k + 1 (same
-  // stream, so launch k - 1, its previous user, has finished).  Own cache lines: every wave
-  // polls `stop` above each iteration.
-  unsigned long long claim[2 * 8];
+  // Sweep work counters (64-nonce wave iterations claimed so far) of the launch's 8 sub-ranges
+  // (one per XCD), for each launch parity: launch k claims from claim[k & 1][*] and zeroes
+  // claim[(k + 1) & 1][*] for launch k + 1 (same stream, so launch k - 1, their previous
+  // user, has finished).  One cache line each: atomics on one address serialise (~18 ns
+  // each), and every wave polls `stop` above each iteration.
+  unsigned long long claim[2 * kClaimRanges * 8];
   unsigned long long done_shard[kDoneShards * 8];  // nonces hashed, one counter per 64-byte line
   uint64_t done() const {
     uint64_t s = 0;

@@ -172,31 +172,44 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
     const uint64_t stride = (uint64_t)gridDim.x * kBlock;
     for (uint64_t ib = wave0; ib < a.count; ib += stride) step(ib);
   } else {
-    // Sweep: waves claim runs of 64-nonce iterations from the launch's counter (guided
-    // self-scheduling: a claim takes remaining / (2 W) iterations, at least 1, at most
-    // max_claim).  VALU issue favours a SIMD's oldest wave, so with a fixed per-wave share
-    // the young waves finish late and the launch ends in a tail with one or two waves per
-    // SIMD; claiming keeps every SIMD full until the range is used up.
-    unsigned long long* ctr = &st->claim[(a.claim_slot & 1) * 8];
-    if (blockIdx.x == 0 && threadIdx.x == 0)
-      __hip_atomic_store(&st->claim[((a.claim_slot + 1) & 1) * 8], 0ull, __ATOMIC_RELAXED,
+    // Sweep: waves claim runs of 64-nonce iterations from counters instead of owning a fixed
+    // share.  VALU issue favours a SIMD's oldest wave, so with fixed shares the young waves
+    // finish late and the launch ends in a tail with one or two waves per SIMD; claiming keeps
+    // every SIMD full until the range is used up.  The launch's T iterations are split into 8
+    // sub-ranges with one counter each (atomics on ONE address serialise at ~18 ns: 8,192 waves
+    // claiming 8 iterations at a time halve the throughput); a wave starts on its XCD's
+    // sub-range (workgroups are dealt to XCDs round-robin) and then helps the others.  Claim
+    // size = remaining / (2 x waves per sub-range), between 1 and max_claim (guided
+    // self-scheduling, capped because a young wave is several times slower than an old one).
+    const uint32_t slot = a.claim_slot & 1;
+    if (blockIdx.x == 0 && threadIdx.x < kClaimRanges)
+      __hip_atomic_store(&st->claim[((1 - slot) * kClaimRanges + threadIdx.x) * 8], 0ull, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t T = (a.count + 63) >> 6;                    // wave iterations in the launch
-    const uint64_t W2 = 2ull * gridDim.x * (kBlock / 64);      // 2 x waves in the launch
-    uint64_t seen = 0;                                         // counter value at the last claim
-    for (;;) {
-      const uint64_t left = T > seen ? T - seen : 0;
-      uint64_t n = left / W2;
-      n = n < 1 ? 1 : (n > a.max_claim ? a.max_claim : n);
-      uint64_t c = 0;
-      if (lane == 0) c = atomicAdd(ctr, (unsigned long long)n);
-      c = readlane64(c, 0);
-      if (c >= T) break;
-      seen = c + n;
-      const uint64_t end = seen < T ? seen : T;
-      bool go = true;
-      for (uint64_t k = c; k < end && go; ++k) go = step(k << 6);
-      if (!go) break;
+    const uint64_t T = (a.count + 63) >> 6;                                  // wave iterations
+    const uint64_t W2 = 2ull * gridDim.x * (kBlock / 64) / kClaimRanges;     // 2 x waves per sub-range
+    const uint32_t home = blockIdx.x % kClaimRanges;
+    bool go = true;
+    for (uint32_t k = 0; k < kClaimRanges && go; ++k) {
+      const uint32_t x = (home + k) % kClaimRanges;
+      const uint64_t lo = T * x / kClaimRanges, Tx = T * (x + 1) / kClaimRanges - lo;
+      unsigned long long* ctr = &st->claim[(slot * kClaimRanges + x) * 8];
+      uint64_t seen = 0;  // the counter as last seen by this wave
+      if (k) {            // helping: start from the counter's current value (it may be nearly used up)
+        uint64_t cur = 0;
+        if (lane == 0) cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        seen = readlane64(cur, 0);
+      }
+      while (go && seen < Tx) {
+        uint64_t n = (Tx - seen) / W2;
+        n = n < 1 ? 1 : (n > a.max_claim ? a.max_claim : n);
+        uint64_t c = 0;
+        if (lane == 0) c = atomicAdd(ctr, (unsigned long long)n);
+        c = readlane64(c, 0);
+        if (c >= Tx) break;
+        seen = c + n;
+        const uint64_t end = seen < Tx ? seen : Tx;
+        for (uint64_t it = c; it < end && go; ++it) go = step((lo + it) << 6);
+      }
     }
   }
   if (lane == 0 && done) atomicAdd(&st->done_shard[(blockIdx.x % kDoneShards) * 8], (unsigned long long)done);
