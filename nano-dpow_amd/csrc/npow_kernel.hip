@@ -10,22 +10,23 @@
 //    generation time (11 of 16 message words are zero).  Every nonce-independent
 //    intermediate (round 1's three column steps and more) is computed once per
 //    root on the host and arrives in SGPRs.  Round 12's dead half is removed.
-//  * 64-bit adds are single `v_lshl_add_u64` instructions (measured: one
-//    64-bit add per 4.4 SIMD cycles, the cost of ONE v_add_co_u32, half the
-//    v_add_co/v_addc pair -- profiles/r01_valu_ubench.json).
+//  * 64-bit adds are single `v_lshl_add_u64` instructions (half rate, 4 SIMD cycles
+//    for the whole add; the v_add_co/v_addc carry pair serialises the wave on VCC --
+//    DESIGN.md section 4, profiles/r01_valu_mix2_timebudget.jsonl).
 //  * Rotations are split into 32-bit halves: rotr32 is a free register swap
-//    folded into the xor that feeds it, rotr24 / rotr16 / rotr63 are two
-//    `v_alignbit_b32` each.
-//  * Grid-stride loop over the launch's nonce range; the hit test is a wave
-//    ballot, so a wave leaves the fast path only when one of its 64 lanes wins.
+//    folded into the xor that feeds it, rotr24 / rotr16 are two `v_alignbit_b32`,
+//    rotr63 is `v_lshrrev_b32` + `v_lshl_add_u64 x, 1, {hi >> 31, 0}`.
+//  * The hit test is a wave ballot, so a wave leaves the fast path only when one of
+//    its 64 lanes wins.
 //  * First-win search (npow_pool_kernel): every live job of the device's work
 //    pool in one launch; first win per job by atomicMax on its slot's dead word,
 //    published to a host-coherent mailbox with system-scope stores; every wave
 //    polls its slot's dead word each iteration (agent-scope load, L2) and the
-//    host kill word every poll_mask+1 iterations (system-scope load).
-//  * Sweep (npow_task_kernel<kSweep>): every hit appended through an atomic
-//    counter (order-free; the host sorts).  Values mode: writes every value
-//    (parity tests).
+//    host kill / yield words every poll_mask+1 iterations (system-scope loads); a
+//    launch ends on a wall-clock budget read from s_memrealtime.
+//  * Sweep (npow_task_kernel<kSweep>): waves claim runs of iterations from 8
+//    per-XCD counters; every hit appended through an atomic counter (order-free;
+//    the host sorts).  Values mode: grid-stride, writes every value (parity tests).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
