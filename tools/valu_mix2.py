@@ -39,7 +39,33 @@ PATTERNS = {
                                        "xor", "xor", "alignbyte", "alignbyte", "addco", "addc", "xor", "xor",
                                        "lshr", "lshlor", "lshr", "lshlor"],
     "add64 sgpr": ["addsgpr"],
+    "chain xor": ("chain", ["xor"]), "chain xor|align": ("chain", ["xor", "align"]),
+    "chain xor|add64": ("chain", ["xor", "add64"]), "chain xor xor|add64": ("chain", ["xor", "xor", "add64"]),
+    "chain G-like mix": ("chain", PATTERNS_ALL["G-like mix"]),
 }
+
+
+def emit_chain(kinds, n):
+    """The kinds in order, each instruction reading the previous one's result as src0 (a
+    dependent chain, as in the generated stream's `seq` order), destinations rotating over
+    even registers v8..v38."""
+    out, prev = [], 40
+    for i in range(n):
+        k = kinds[i % len(kinds)]
+        d = 8 + (i * 2) % 32
+        s1 = 52 + (i * 2) % 12
+        if k == "xor":
+            out.append(f"v_xor_b32_e64 v{d}, v{prev}, v{s1}")
+        elif k == "align":
+            out.append(f"v_alignbit_b32 v{d}, v{prev}, v{s1}, 24")
+        elif k == "add64":
+            out.append(f"v_lshl_add_u64 v[{d}:{d + 1}], v[{prev}:{prev + 1}], 0, v[{s1}:{s1 + 1}]")
+        elif k == "lshr":
+            out.append(f"v_lshrrev_b32_e64 v{d}, 31, v{prev}")
+        else:
+            raise ValueError(k)
+        prev = d
+    return out
 
 
 def emit2(kind, i):
@@ -117,6 +143,8 @@ def main():
     for k, (name, pat) in enumerate(items):
         if pat is None or isinstance(pat, str):
             lines = real_stream(pat)
+        elif isinstance(pat, tuple):  # ("chain", kinds)
+            lines = emit_chain(pat[1], n_body)
         else:
             lines = [emit2(pat[i % len(pat)], i) for i in range(n_body)]
         n_ins = sum(1 for ln in lines if ln.startswith("v_"))
