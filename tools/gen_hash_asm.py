@@ -261,10 +261,11 @@ def lower(dag: Dag, out: Node):
 
 # issue cost (SIMD cycles per wave64 instruction, profiles/r01_valu_ubench.json) and latency model
 COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b32": 4.3, "v_lshl_add_u64": 4.4,
-        "v_lshrrev_b32": 2.5, "v_mov_b32": 2.4, "v_add_co_u32": 2.1, "v_addc_co_u32": 2.1}
+        "v_lshrrev_b32": 2.5, "v_mov_b32": 2.4, "v_add_co_u32": 2.1, "v_addc_co_u32": 2.1, "v_mad_u32_u24": 4.0}
 # 64-bit add as v_add_co_u32 + v_addc_co_u32 (carry through VCC) instead of one v_lshl_add_u64:
 # both issue at full rate next to xors (profiles/r01_valu_mix2.jsonl), v_lshl_add_u64 does not
 ADD_CC = False
+ROT_MAD = lambda n, h: False  # which rotr16/24 halves use v_lshrrev_b32 + v_mad_u32_u24 (--rotmad)
 ROTL1_CC = False  # rotr63 = x + x + carry as v_add_co_u32 + 2x v_addc_co_u32
 ROTL1_VIA_ADD = True  # rotr63 = (x << 1) + (x >> 63): v_lshrrev_b32 + v_lshl_add_u64 with a zero partner
 # Measured on MI355X (tools/valu_patterns.py): in a stream that mixes in 64-bit / 3-operand VALU
@@ -543,19 +544,25 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             r = al.take2(avoid=(tl, th))
             loc[op.dst.id] = r
             n = op.n
-            if n < 32:
-                lines.append(f"v_alignbit_b32 v{r}, v{th}, v{tl}, {n}")
-                lines.append(f"v_alignbit_b32 v{r + 1}, v{tl}, v{th}, {n}")
-            else:
-                k = n - 32
-                lines.append(f"v_alignbit_b32 v{r}, v{tl}, v{th}, {k}")
-                lines.append(f"v_alignbit_b32 v{r + 1}, v{th}, v{tl}, {k}")
+            cnt("v_xor_b32")
+            cnt("v_xor_b32")
+            # half h of rotr_n: (x_h >> n) | (x_other << (32 - n)) -- one v_alignbit_b32, or
+            # v_lshrrev_b32 + v_mad_u32_u24 (x_other[23:0] * 2^(32-n) + (x_h >> n); exact for
+            # n = 16, 24), which runs in the multiplier next to alignbit / v_lshl_add_u64
+            for h, (xa, xb) in enumerate(((tl, th), (th, tl))):
+                if n < 32 and n in (16, 24) and ROT_MAD(n, h):
+                    lines.append(f"v_lshrrev_b32 v{r + h}, {n}, v{xa}")
+                    lines.append(f"v_mad_u32_u24 v{r + h}, v{xb}, %[k{32 - n}], v{r + h}")
+                    cnt("v_lshrrev_b32")
+                    cnt("v_mad_u32_u24")
+                elif n < 32:
+                    lines.append(f"v_alignbit_b32 v{r + h}, v{xb}, v{xa}, {n}")
+                    cnt("v_alignbit_b32")
+                else:
+                    lines.append(f"v_alignbit_b32 v{r + h}, v{xa}, v{xb}, {n - 32}")
+                    cnt("v_alignbit_b32")
             al.release(tl)
             al.release(th)
-            cnt("v_xor_b32")
-            cnt("v_xor_b32")
-            cnt("v_alignbit_b32")
-            cnt("v_alignbit_b32")
         elif op.kind == "xor":
             s0l, s1l = xor_operands(a, b, 0)
             s0h, s1h = xor_operands(a, b, 1)
@@ -824,7 +831,7 @@ def allocate_and_emit(order: List[Ins], vrs: List[VR], base: int, limit: int, vo
 # A tiny interpreter of the emitted text, to check the generator itself against hashlib.
 def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
     regs: Dict[int, int] = {}
-    named: Dict[str, int] = {"nonce_lo": nonce & M32, "nonce_hi": nonce >> 32}
+    named: Dict[str, int] = {"nonce_lo": nonce & M32, "nonce_hi": nonce >> 32, "k8": 1 << 8, "k16": 1 << 16}
     for i, u in enumerate(uni_vals):
         named[f"u{i}_lo"] = u & M32
         named[f"u{i}_hi"] = u >> 32
@@ -874,6 +881,8 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
             wr32(ops[0], rd32(ops[2]) >> int(ops[1]))
         elif opc == "v_mov_b32":
             wr32(ops[0], rd32(ops[1]))
+        elif opc == "v_mad_u32_u24":
+            wr32(ops[0], (rd32(ops[1]) & 0xffffff) * (rd32(ops[2]) & 0xffffff) + rd32(ops[3]))
         elif opc == "v_add_co_u32":
             assert ops[1] == "vcc"
             t = rd32(ops[2]) + rd32(ops[3])
@@ -952,9 +961,10 @@ def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List
     if "vcc" in text:
         clobbers += ', "vcc"'
     ops_in = []
-    for nm, expr in [("nonce", "nonce"), ("nonce_lo", "(uint32_t)nonce"), ("nonce_hi", "(uint32_t)(nonce >> 32)")]:
+    for nm, expr in [("nonce", "nonce"), ("nonce_lo", "(uint32_t)nonce"), ("nonce_hi", "(uint32_t)(nonce >> 32)"),
+                     ("k8", "256u"), ("k16", "65536u")]:
         if f"%[{nm}]" in text:
-            ops_in.append(f'[{nm}] "v"({expr})')
+            ops_in.append(f'[{nm}] "{"s" if nm.startswith("k") else "v"}"({expr})')
     for i in range(nu):
         if f"%[u{i}]" in text:
             ops_in.append(f'[u{i}] "s"(u[{i}])')
@@ -1016,6 +1026,8 @@ def main() -> int:
                          "v_add_co_u32 + 2x v_addc_co_u32 carry chain (cc)")
     ap.add_argument("--add", choices=["u64", "cc"], default="u64",
                     help="64-bit add as one v_lshl_add_u64 (u64) or v_add_co_u32 + v_addc_co_u32 (cc)")
+    ap.add_argument("--rotmad", choices=["none", "lo", "hi", "both", "r16", "r24", "r16lo", "r24lo"], default="none",
+                    help="rotr16/rotr24 halves as v_lshrrev_b32 + v_mad_u32_u24 instead of v_alignbit_b32")
     ap.add_argument("--enc", choices=["vop3", "vop2"], default="vop3",
                     help="encoding of the simple 32-bit ops (xor, lshrrev)")
     ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
@@ -1024,6 +1036,10 @@ def main() -> int:
     args = ap.parse_args()
     global ROTL1_VIA_ADD, VOP3_SIMPLE, SWAP_MOV, PAD, ADD_CC, ROTL1_CC
     ADD_CC = args.add == "cc"
+    global ROT_MAD
+    ROT_MAD = {"none": lambda n, h: False, "lo": lambda n, h: h == 0, "hi": lambda n, h: h == 1,
+               "both": lambda n, h: True, "r16": lambda n, h: n == 16, "r24": lambda n, h: n == 24,
+               "r16lo": lambda n, h: n == 16 and h == 0, "r24lo": lambda n, h: n == 24 and h == 0}[args.rotmad]
     SWAP_MOV = args.swapmov
     PAD = {"odd": ['.p2align 3', 's_nop 0'], "even": ['.p2align 3'], "none": []}[args.pad]
     ROTL1_VIA_ADD = args.rotl1 == "add"
@@ -1062,7 +1078,8 @@ def main() -> int:
             print(f"MISMATCH root={root.hex()} nonce={nonce:016x} got={got:016x} want={want:016x}")
             return 1
     host_prog = c_expr_program(frontier)
-    write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --add {args.add} --enc {args.enc}" + (" --swapmov" if args.swapmov else "")
+    write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --add {args.add} --enc {args.enc}"
+              + (f" --rotmad {args.rotmad}" if args.rotmad != "none" else "") + (" --swapmov" if args.swapmov else "")
               + (f" --lat {args.lat:g} --window {args.window}" if args.sched == "ilp" else "") + f" --pad {args.pad}", est)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
           f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")

@@ -39,6 +39,29 @@ PATTERNS = {
                                        "xor", "xor", "alignbyte", "alignbyte", "addco", "addc", "xor", "xor",
                                        "lshr", "lshlor", "lshr", "lshlor"],
     "add64 sgpr": ["addsgpr"],
+    "mul24": ["mul24"], "mul24k": ["mul24k"], "mad24": ["mad24"], "mad24s": ["mad24s"], "mad16": ["mad16"],
+    "lshl e64": ["lshlk"], "lshr24 e64": ["lshr8"],
+    "xor|mad24s alt": ["xor", "mad24s"], "lshr|mad24s alt": ["lshr8", "mad24s"],
+    "G rot via mad24": ["xor", "xor", "lshr8", "mad24s", "lshr8", "mad24s", "add64", "xor", "xor", "add64"],
+    "G rot via align": ["xor", "xor", "align", "align", "add64", "xor", "xor", "add64"],
+    "P2 mad->align": ["xor", "xor", "lshr8", "align", "lshr8", "align", "add64", "xor", "xor", "add64"],
+    "P3 lshr->xor": ["xor", "xor", "xor", "mad24s", "xor", "mad24s", "add64", "xor", "xor", "add64"],
+    "P4 mad->add64": ["xor", "xor", "lshr8", "add64", "lshr8", "add64", "add64", "xor", "xor", "add64"],
+    "P5 lshr->xor mad->align": ["xor", "xor", "xor", "align", "xor", "align", "add64", "xor", "xor", "add64"],
+    "P6 FFFHFHHFFH all xor/align": ["xor", "xor", "xor", "align", "xor", "align", "align", "xor", "xor", "align"],
+    "P7 FFFHFHHFFH mad only": ["xor", "xor", "xor", "mad24s", "xor", "mad24s", "mad24s", "xor", "xor", "mad24s"],
+    "P8 lshr|align alt": ["lshr8", "align"],
+    "P9 lshr|add64 alt": ["lshr8", "add64"],
+    "P10 lshr|mad24s": ["lshr8", "mad24s"],
+    "P11 xor|mad24s": ["xor", "mad24s"],
+    "P12 FFHH xor/mad": ["xor", "xor", "mad24s", "mad24s"],
+    "P13 FFHH xor/align": ["xor", "xor", "align", "align"],
+    "Q1 mad24s|add64": ["mad24s", "add64"], "Q2 mad24s|align": ["mad24s", "align"],
+    "Q3 mad24|add64": ["mad24", "add64"], "Q4 mul24|add64": ["mul24", "add64"],
+    "Q5 lshl|add64": ["lshlk", "add64"], "Q6 mad24s|add64|xor|xor": ["mad24s", "add64", "xor", "xor"],
+    "Q7 align|add64|xor|xor": ["align", "add64", "xor", "xor"], "Q8 mad24s|xor|add64|xor": ["mad24s", "xor", "add64", "xor"],
+    "Q9 lshl|align": ["lshlk", "align"], "Q10 mul24|align": ["mul24", "align"],
+    "Q11 add64 sgpr|align": ["addsgpr", "align"], "Q12 mad24s|lshl": ["mad24s", "lshlk"],
     "chain xor": ("chain", ["xor"]), "chain xor|align": ("chain", ["xor", "align"]),
     "chain xor|add64": ("chain", ["xor", "add64"]), "chain xor xor|add64": ("chain", ["xor", "xor", "add64"]),
     "chain G-like mix": ("chain", PATTERNS_ALL["G-like mix"]),
@@ -104,6 +127,20 @@ def emit2(kind, i):
         return f"v_add_u32 v{d}, v{s0}, v{s1}"
     if kind == "addsgpr":
         return f"v_lshl_add_u64 v[{d}:{d + 1}], v[{s0}:{s0 + 1}], 0, s[40:41]"
+    if kind == "mul24":
+        return f"v_mul_u32_u24_e64 v{d}, v{s0}, s40"
+    if kind == "mul24k":
+        return f"v_mul_u32_u24 v{d}, 0x100, v{s0}"
+    if kind == "mad24":
+        return f"v_mad_u32_u24 v{d}, v{s0}, 8, v{s1}"
+    if kind == "mad24s":
+        return f"v_mad_u32_u24 v{d}, v{s0}, s40, v{s1}"
+    if kind == "mad16":
+        return f"v_mad_u32_u16 v{d}, v{s0}, s40, v{s1}"
+    if kind == "lshlk":
+        return f"v_lshlrev_b32_e64 v{d}, 8, v{s0}"
+    if kind == "lshr8":
+        return f"v_lshrrev_b32_e64 v{d}, 24, v{s0}"
     if kind == "add64dep":
         return "v_lshl_add_u64 v[8:9], v[8:9], 0, v[40:41]"
     return emit(kind, i)
@@ -116,6 +153,7 @@ def real_stream(path=None):
     asm = txt[txt.index("  asm(") + 6:txt.index("      : [value_lo]")]
     out = []
     for ln in re.findall(r'"(.*?)\\n"', asm):
+        ln = ln.replace("%[k8]", "s38").replace("%[k16]", "s39")
         ln = ln.replace("%[nonce_lo]", "v56").replace("%[nonce_hi]", "v57")
         ln = ln.replace("%[nonce]", "v[56:57]").replace("%[value_lo]", "v58").replace("%[value_hi]", "v59")
         ln = re.sub(r"%\[u(\d+)_lo\]", lambda m: f"s{40 + 2 * int(m.group(1)) % 30}", ln)
@@ -130,7 +168,7 @@ def main():
     budget_us = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
     n_body = 360
     clob = ", ".join(f'"v{r}"' for r in range(8, 64))
-    sclob = ", ".join(f'"s{r}"' for r in range(40, 70))
+    sclob = ", ".join(f'"s{r}"' for r in range(38, 70))
     kernels, runs = [], []
     items = list(PATTERNS.items()) + [("real hash stream", None)]
     # extra generated streams: MIX_STREAMS="name=path.inc,name2=path2.inc"
