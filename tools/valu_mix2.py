@@ -62,6 +62,9 @@ PATTERNS = {
     "Q7 align|add64|xor|xor": ["align", "add64", "xor", "xor"], "Q8 mad24s|xor|add64|xor": ["mad24s", "xor", "add64", "xor"],
     "Q9 lshl|align": ["lshlk", "align"], "Q10 mul24|align": ["mul24", "align"],
     "Q11 add64 sgpr|align": ["addsgpr", "align"], "Q12 mad24s|lshl": ["mad24s", "lshlk"],
+    "mad64": ["mad64"], "mad64n": ["mad64n"], "mullo": ["mullo"], "mulhi24": ["mulhi24"],
+    "mad64|align": ["mad64", "align"], "mad64|add64": ["mad64", "add64"], "mad64|xor": ["mad64", "xor"],
+    "mad64n|align": ["mad64n", "align"], "mulhi24|align": ["mulhi24", "align"],
     "chain xor": ("chain", ["xor"]), "chain xor|align": ("chain", ["xor", "align"]),
     "chain xor|add64": ("chain", ["xor", "add64"]), "chain xor xor|add64": ("chain", ["xor", "xor", "add64"]),
     "chain G-like mix": ("chain", PATTERNS_ALL["G-like mix"]),
@@ -141,6 +144,14 @@ def emit2(kind, i):
         return f"v_lshlrev_b32_e64 v{d}, 8, v{s0}"
     if kind == "lshr8":
         return f"v_lshrrev_b32_e64 v{d}, 24, v{s0}"
+    if kind == "mad64":
+        return f"v_mad_u64_u32 v[{d}:{d + 1}], s[20:21], v{s0}, v{s1}, v[{s1}:{s1 + 1}]"
+    if kind == "mad64n":  # carry-out to a rotating SGPR pair
+        return f"v_mad_u64_u32 v[{d}:{d + 1}], s[{20 + (i * 2) % 8}:{21 + (i * 2) % 8}], v{s0}, 1, v[{s1}:{s1 + 1}]"
+    if kind == "mullo":
+        return f"v_mul_lo_u32 v{d}, v{s0}, v{s1}"
+    if kind == "mulhi24":
+        return f"v_mul_hi_u32_u24_e64 v{d}, v{s0}, v{s1}"
     if kind == "add64dep":
         return "v_lshl_add_u64 v[8:9], v[8:9], 0, v[40:41]"
     return emit(kind, i)
@@ -194,7 +205,7 @@ __global__ __launch_bounds__(256) void mix_{k}(unsigned long long* out) {{
   const unsigned long long m0 = __builtin_amdgcn_s_memtime();
   asm volatile("v_mov_b32 v40, v0\\n\\tv_mov_b32 v52, v0\\n\\tv_mov_b32 v56, v0\\n\\tv_mov_b32 v57, 0" ::: {clob});
   do {{
-    asm volatile("{asm}" ::: {clob}, {sclob}, "vcc");
+    asm volatile("{asm}" ::: {clob}, {sclob}, "vcc", "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
     ++n;
     asm volatile("s_memrealtime %0\\n\\ts_waitcnt lgkmcnt(0)" : "=s"(now) :: "memory");
   }} while (now - t0 < {budget_us * 100}ull);
