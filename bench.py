@@ -294,12 +294,90 @@ def workload_sweep(eng, args, rank, world, dist):
     return line
 
 
+def _burst_http(eng, args, rank, world, dist):
+    """BASELINE config 4 at the JSON boundary: --roots concurrent work_generate POSTs to the HTTP
+    work server (one connection each), 25 % answered by a work_cancel POST at a uniform time in
+    [0, 0.5 x the expected burst time); every work reply re-validated (npow_work_value), every
+    cancelled request must answer {"error": "Cancelled"} unless its work was already found."""
+    import random
+    import threading
+    import urllib.request
+    from nanopow.server import HttpWorkServer, WorkServer
+    n = args.roots
+    rng = random.Random(4343 + rank)
+    idx = [9_000_000 + rank * 1_000_000 + i for i in range(n)]
+    roots = [bench_root(i) for i in idx]
+    cancel_set = set(rng.sample(range(n), n // 4))
+    est = n * float(1 << 29) / (25e9 * max(1, eng.n_devices if world == 1 else 1))
+    cancel_at = sorted((rng.uniform(0.0, 0.5 * est), i) for i in cancel_set)
+    srv = HttpWorkServer(WorkServer(eng, max_active=64, device_mask=0 if world == 1 else 1), "127.0.0.1", 0).start()
+
+    def post(obj, timeout=600):
+        req = urllib.request.Request(f"http://{srv.address}", data=json.dumps(obj).encode(), method="POST",
+                                     headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=timeout) as r:
+            return json.loads(r.read())
+    replies, done_at = [None] * n, [0.0] * n
+    eng.reset_stats(0)
+    if dist is not None:
+        dist.barrier()
+    t0 = time.perf_counter()
+
+    def client(i):
+        replies[i] = post({"action": "work_generate", "hash": roots[i].hex().upper(), "difficulty": f"{SEND:016x}"})
+        done_at[i] = time.perf_counter() - t0
+
+    finished = threading.Event()
+
+    def canceller():
+        for t_c, i in cancel_at:
+            if finished.wait(max(0.0, t0 + t_c - time.perf_counter())):
+                return  # every request has been answered
+            post({"action": "work_cancel", "hash": roots[i].hex().upper()})
+    try:
+        ths = [threading.Thread(target=client, args=(i,)) for i in range(n)]
+        for t in ths:
+            t.start()
+        th_c = threading.Thread(target=canceller, daemon=True)
+        th_c.start()
+        for t in ths:
+            t.join()
+        wall = time.perf_counter() - t0
+        finished.set()
+        th_c.join(60)
+    finally:
+        srv.stop()
+    ok = [i for i in range(n) if "work" in replies[i]]
+    bad = [i for i in ok if eng.work_value(roots[i], int(replies[i]["work"], 16)) < SEND]
+    wrong_err = [i for i in range(n) if "work" not in replies[i]
+                 and (i not in cancel_set or replies[i].get("error") != "Cancelled")]
+    st = eng.stats(0)
+    ttw = [done_at[i] for i in ok]
+    nonces, wall, ttw, (kms, kn, nl, n_bad, n_we) = _reduce(dist, st.nonces, wall, ttw,
+                                                            (st.kernel_ms, st.nonces, st.launches, len(bad),
+                                                             len(wrong_err)))
+    line = result_line(world, n, 0, nonces, wall, ttw or [0.0], kms, kn, nl)
+    line["config"] = {"workload": f"BASELINE configs[3]: burst of {n} concurrent work_generate requests per GPU "
+                                  "at fffffff800000000 POSTed to the HTTP work server, 25 % answered by work_cancel",
+                      "threshold": "fffffff800000000", "roots_per_gpu": n, "boundary": "JSON over HTTP (127.0.0.1)",
+                      "parallelism": f"dp{world} (disjoint roots per GPU)" if world > 1 else
+                                     f"work pool over {eng.n_devices} GPU(s)"}
+    line["burst"] = {"ok": len(ok), "cancelled_requested": len(cancel_set),
+                     "cancel_lost_race": sum(1 for i in cancel_set if "work" in replies[i]),
+                     "invalid_replies": int(n_bad), "unexpected_errors": int(n_we)}
+    if n_bad or n_we:
+        raise RuntimeError(f"burst/http: {int(n_bad)} invalid replies, {int(n_we)} unexpected errors")
+    return line
+
+
 def workload_burst(eng, args, rank, world, dist):
     """BASELINE config 4: a burst of --roots concurrent requests with 25 % mid-search cancels."""
     import queue
     import random
     import threading
     from nanopow import _lib
+    if args.via == "http":
+        return _burst_http(eng, args, rank, world, dist)
     n = args.roots
     rng = random.Random(4242 + rank)
     idx = [7_000_000 + rank * 1_000_000 + i for i in range(n)]
@@ -589,6 +667,8 @@ def main() -> int:
     ap.add_argument("--rate", type=float, default=20.0, help="dpow: work messages per second")
     ap.add_argument("--concurrency", type=int, default=1, help="dpow: WorkHandler loops (reference: 1)")
     ap.add_argument("--cpu-requests", type=int, default=4, help="receive: requests timed on the CPU reference")
+    ap.add_argument("--via", choices=["abi", "http"], default="abi",
+                    help="burst: submit through the C ABI work pool or POST to the HTTP work server")
     ap.add_argument("--http-requests", type=int, default=100,
                     help="search, N=1: work_generate requests timed at the JSON boundary after the timed steps")
     args = ap.parse_args()

@@ -308,13 +308,20 @@ class _Handler(BaseHTTPRequestHandler):
         self._send(405, {"error": "Can only POST requests"})
 
 
+class _Listener(ThreadingHTTPServer):
+    # socketserver's default listen backlog is 5: a burst of concurrent work_generate
+    # connections (many clients, or one client's precache wave) would overflow it and wait
+    # out TCP's 1-s SYN retry.
+    request_queue_size = 1024
+
+
 class HttpWorkServer:
     """WorkServer behind a threaded HTTP/1.1 listener (one thread per connection)."""
 
     def __init__(self, work_server: WorkServer, host: str = "127.0.0.1", port: int = 7000) -> None:
         handler = type("Handler", (_Handler,), {"work_server": work_server})
         self.work_server = work_server
-        self.httpd = ThreadingHTTPServer((host, port), handler)
+        self.httpd = _Listener((host, port), handler)
         self.httpd.daemon_threads = True
         self._thread: Optional[threading.Thread] = None
 
