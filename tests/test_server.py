@@ -235,3 +235,32 @@ def test_concurrent_requests_share_the_pool():
         assert post(srv.address, {"action": "status"}) == {"generating": "0", "queue_size": "0"}
     finally:
         srv.stop()
+
+
+def test_burst_of_concurrent_connections_is_accepted_at_once():
+    """300 clients connect at the same moment (a precache wave from many DPoW clients): the
+    listener's backlog holds them all, so no request waits out TCP's 1-s SYN retry."""
+    eng = OracleEngine(chunk=1 << 12, delay=0.0)
+    srv = HttpWorkServer(WorkServer(eng, max_active=64), "127.0.0.1", 0).start()
+    n = 300
+    lat, out = [0.0] * n, [None] * n
+    go = threading.Event()
+
+    def client(i):
+        go.wait()
+        t = time.perf_counter()
+        out[i] = post(srv.address, {"action": "work_generate", "hash": f"{i + 1:064X}", "difficulty": "ff00000000000000"},
+                      timeout=60)
+        lat[i] = time.perf_counter() - t
+    try:
+        ths = [threading.Thread(target=client, args=(i,)) for i in range(n)]
+        for t in ths:
+            t.start()
+        go.set()
+        for t in ths:
+            t.join()
+    finally:
+        srv.stop()
+    for i in range(n):
+        assert oracle.work_value(bytes.fromhex(f"{i + 1:064X}"), int(out[i]["work"], 16)) >= 0xff00000000000000
+    assert max(lat) < 0.9, sorted(lat)[-5:]
