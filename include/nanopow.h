@@ -44,6 +44,8 @@ extern "C" {
 #define NPOW_ERR_HIP (-4)
 #define NPOW_ERR_INVALID_WORK (-5) /* GPU result failed CPU re-validation 3 times in a row */
 #define NPOW_ERR_CAPACITY (-6)     /* sweep found more hits than `cap` (n_out still exact) */
+#define NPOW_ERR_INTERNAL (-7)     /* host-side failure (out of memory, thread creation); no C++
+                                      exception ever crosses this ABI */
 
 /* Per-device counters; kernel_ms is measured with HIP events recorded on the
  * stream each kernel is launched on (bench.py's roofline leg reads these). */

@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <exception>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -139,9 +140,33 @@ void run_on_devices(const std::vector<Device*>& devs, F&& fn) {
     return;
   }
   std::vector<std::thread> th;
+  std::vector<std::exception_ptr> errs(devs.size());
   th.reserve(devs.size());
-  for (size_t k = 0; k < devs.size(); ++k) th.emplace_back([&, k] { fn(k, *devs[k]); });
+  for (size_t k = 0; k < devs.size(); ++k)
+    th.emplace_back([&, k] {
+      try {
+        fn(k, *devs[k]);
+      } catch (...) {  // an exception may not leave a std::thread: hand it to the caller
+        errs[k] = std::current_exception();
+      }
+    });
   for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+}
+
+// Every extern "C" entry point is a function-try-block: no C++ exception (std::bad_alloc,
+// std::system_error from thread creation, ...) may cross the C ABI.
+int guard_exception() {
+  try {
+    throw;
+  } catch (const std::bad_alloc&) {
+    return fail(NPOW_ERR_INTERNAL, "out of host memory");
+  } catch (const std::exception& e) {
+    return fail(NPOW_ERR_INTERNAL, std::string("host-side failure: ") + e.what());
+  } catch (...) {
+    return fail(NPOW_ERR_INTERNAL, "host-side failure");
+  }
 }
 
 int check_init() {
@@ -220,7 +245,7 @@ const char* npow_version(void) {
   return "libnanopow 0.1 (gfx950 HIP kernel: blake2b-64 nonce search; v_lshl_add_u64 adds, v_alignbit rotations)";
 }
 
-int npow_init(int* n_devices) {
+int npow_init(int* n_devices) try {
   std::lock_guard<std::mutex> g(g_mu);
   if (g_init) {
     if (n_devices) *n_devices = (int)g_devs.size();
@@ -278,9 +303,9 @@ int npow_init(int* n_devices) {
   }
   if (n_devices) *n_devices = (int)g_devs.size();
   return NPOW_OK;
-}
+} catch (...) { return guard_exception(); }
 
-void npow_shutdown(void) {
+void npow_shutdown(void) try {
   std::lock_guard<std::mutex> g(g_mu);
   if (g_init) pool_stop();
   for (auto& d : g_devs) {
@@ -299,7 +324,7 @@ void npow_shutdown(void) {
   }
   g_devs.clear();
   g_init = false;
-}
+} catch (...) { (void)guard_exception(); }
 
 uint64_t npow_work_value(const uint8_t root[32], uint64_t nonce) {
   uint64_t m[4];
@@ -307,7 +332,7 @@ uint64_t npow_work_value(const uint8_t root[32], uint64_t nonce) {
   return host_work_value(m, nonce);
 }
 
-int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t blocks_per_cu) {
+int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t blocks_per_cu) try {
   if (iters_per_launch) {
     if (iters_per_launch > 65536) return fail(NPOW_ERR_BAD_ARGUMENT, "iters_per_launch must be <= 65536");
     g_iters = iters_per_launch;
@@ -318,17 +343,17 @@ int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t 
     g_blocks_per_cu = blocks_per_cu;
   }
   return NPOW_OK;
-}
+} catch (...) { return guard_exception(); }
 
-int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu) {
+int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu) try {
   if (budget_us != 0xffffffffu && budget_us > 1000000) return fail(NPOW_ERR_BAD_ARGUMENT, "budget_us must be <= 1000000");
   if (blocks_per_cu > 32) return fail(NPOW_ERR_BAD_ARGUMENT, "blocks_per_cu must be <= 32");
   if (budget_us != 0xffffffffu) g_budget_us = budget_us;
   if (blocks_per_cu) g_pool_blocks_per_cu = blocks_per_cu;
   return NPOW_OK;
-}
+} catch (...) { return guard_exception(); }
 
-int npow_device_stats_get(int device, npow_device_stats* out) {
+int npow_device_stats_get(int device, npow_device_stats* out) try {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size() || !out) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
   Device& d = *g_devs[device];
@@ -340,9 +365,9 @@ int npow_device_stats_get(int device, npow_device_stats* out) {
   out->cus = d.cus;
   out->grid = pool_grid_of(d);
   return NPOW_OK;
-}
+} catch (...) { return guard_exception(); }
 
-int npow_device_stats_reset(int device) {
+int npow_device_stats_reset(int device) try {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size()) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
   Device& d = *g_devs[device];
@@ -350,21 +375,21 @@ int npow_device_stats_reset(int device) {
   d.launches = d.nonces = d.invalid = 0;
   d.kernel_ms = 0.0;
   return NPOW_OK;
-}
+} catch (...) { return guard_exception(); }
 
 int npow_search(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
                 uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* nonce_out,
-                uint64_t* value_out, uint64_t* nonces_done) {
+                uint64_t* value_out, uint64_t* nonces_done) try {
   if (int rc = check_init()) return rc;
   if (!root || !nonce_out) return fail(NPOW_ERR_BAD_ARGUMENT, "root and nonce_out are required");
   uint64_t ticket = 0;
   if (int rc = pool_submit(root, threshold, start, device_mask, max_nonces_per_device, cancel, &ticket)) return rc;
   return pool_wait(ticket, -1, nonce_out, value_out, nonces_done);
-}
+} catch (...) { return guard_exception(); }
 
 int npow_search_batch(const uint8_t* roots, const uint64_t* thresholds, uint32_t n, uint64_t device_mask,
                       uint64_t max_nonces_per_root, const volatile uint32_t* const* cancel, uint64_t* nonces_out,
-                      uint64_t* values_out, int32_t* status_out, uint64_t* nonces_done) {
+                      uint64_t* values_out, int32_t* status_out, uint64_t* nonces_done) try {
   if (int rc = check_init()) return rc;
   if (nonces_done) *nonces_done = 0;
   if (n == 0) return NPOW_OK;
@@ -405,39 +430,39 @@ int npow_search_batch(const uint8_t* roots, const uint64_t* thresholds, uint32_t
   if (nonces_done) *nonces_done = total;
   if (err != NPOW_OK) return fail(err, err_msg);
   return NPOW_OK;
-}
+} catch (...) { return guard_exception(); }
 
 int npow_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
-                uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket) {
+                uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket) try {
   if (int rc = check_init()) return rc;
   if (!root || !ticket) return fail(NPOW_ERR_BAD_ARGUMENT, "root and ticket are required");
   return pool_submit(root, threshold, start, device_mask, max_nonces_per_device, cancel, ticket);
-}
+} catch (...) { return guard_exception(); }
 
 int npow_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce_out, uint64_t* value_out,
-              uint64_t* nonces_done) {
+              uint64_t* nonces_done) try {
   if (int rc = check_init()) return rc;
   return pool_wait(ticket, timeout_us, nonce_out, value_out, nonces_done);
-}
+} catch (...) { return guard_exception(); }
 
-int npow_cancel(uint64_t ticket) {
+int npow_cancel(uint64_t ticket) try {
   if (int rc = check_init()) return rc;
   return pool_cancel(ticket);
-}
+} catch (...) { return guard_exception(); }
 
-int npow_pool_config(uint32_t max_active) {
+int npow_pool_config(uint32_t max_active) try {
   if (int rc = check_init()) return rc;
   return pool_set_max_active(max_active);
-}
+} catch (...) { return guard_exception(); }
 
-int npow_pool_status(uint32_t* queued, uint32_t* active) {
+int npow_pool_status(uint32_t* queued, uint32_t* active) try {
   if (int rc = check_init()) return rc;
   pool_counts(queued, active);
   return NPOW_OK;
-}
+} catch (...) { return guard_exception(); }
 
 int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t count, uint64_t device_mask,
-               const volatile uint32_t* cancel, uint64_t* out, uint64_t cap, uint64_t* n_out) {
+               const volatile uint32_t* cancel, uint64_t* out, uint64_t cap, uint64_t* n_out) try {
   if (int rc = check_init()) return rc;
   if (!root || !n_out || (cap && !out)) return fail(NPOW_ERR_BAD_ARGUMENT, "root, n_out (and out when cap>0) required");
   auto devs = select_devices(device_mask);
@@ -482,9 +507,9 @@ int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint6
   if (overflow) return fail(NPOW_ERR_CAPACITY, "device hit buffer overflow (more than 2^20 hits per device)");
   if (total > cap) return fail(NPOW_ERR_CAPACITY, "more hits than cap");
   return NPOW_OK;
-}
+} catch (...) { return guard_exception(); }
 
-int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t count, uint64_t* values_out) {
+int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t count, uint64_t* values_out) try {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size() || !root || (count && !values_out))
     return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
@@ -508,9 +533,9 @@ int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t cou
   }
   DevState hs;
   return read_state(d, &hs);
-}
+} catch (...) { return guard_exception(); }
 
-int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, uint32_t n, uint64_t* values_out) {
+int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, uint32_t n, uint64_t* values_out) try {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size() || (n && (!roots || !nonces || !values_out)))
     return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
@@ -540,6 +565,6 @@ int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, 
   (void)hipFree(dn);
   (void)hipFree(dv);
   return rc;
-}
+} catch (...) { return guard_exception(); }
 
 }  // extern "C"

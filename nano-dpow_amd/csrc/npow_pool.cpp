@@ -498,7 +498,13 @@ void Worker::run() {
       continue;
     }
     if (!dev_lock_.owns_lock()) dev_lock_.lock();  // waits behind a sweep / values task on this device
-    if (step() != NPOW_OK) {
+    int rc;
+    try {
+      rc = step();
+    } catch (const std::exception& e) {  // nothing may leave the worker thread
+      rc = fail(NPOW_ERR_INTERNAL, std::string("pool worker: ") + e.what());
+    }
+    if (rc != NPOW_OK) {
       fail_all(last_error());
       if (dev_lock_.owns_lock()) dev_lock_.unlock();
       continue;

@@ -28,6 +28,7 @@ NPOW_ERR_BAD_ARGUMENT = -3
 NPOW_ERR_HIP = -4
 NPOW_ERR_INVALID_WORK = -5
 NPOW_ERR_CAPACITY = -6
+NPOW_ERR_INTERNAL = -7
 
 M64 = (1 << 64) - 1
 
@@ -162,6 +163,9 @@ class CancelToken:
         return ctypes.addressof(self._word)
 
 
+_ORPHANED_CANCEL_WORDS: list = []
+
+
 class Ticket:
     """A submitted search (npow_submit); wait() returns its SearchResult once."""
 
@@ -191,6 +195,20 @@ class Ticket:
     def cancel(self) -> None:
         if self.result is None:
             _check(self.engine.lib.npow_cancel(self.ticket), self.engine.lib)
+
+    def __del__(self) -> None:
+        # An abandoned ticket: cancel its search and collect it, so the engine forgets the job
+        # and stops reading this ticket's cancel word before that word is freed.  A job that
+        # does not end within 10 s keeps its cancel word alive for the life of the process.
+        if self.result is not None or not getattr(self, "ticket", 0):
+            return
+        try:
+            lib = self.engine.lib
+            lib.npow_cancel(self.ticket)
+            if lib.npow_wait(self.ticket, 10_000_000, None, None, None) == NPOW_PENDING:
+                _ORPHANED_CANCEL_WORDS.append(self.cancel_token)
+        except Exception:  # interpreter shutdown: the library may already be gone
+            pass
 
 
 class Engine:

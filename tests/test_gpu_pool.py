@@ -216,3 +216,21 @@ def test_new_job_does_not_wait_for_a_long_launch(gpu_engine):
         assert res.status == _lib.NPOW_CANCELLED and res.nonces_done > 0
     finally:
         gpu_engine.set_pool_tuning(budget_us=20_000)
+
+
+def test_abandoned_ticket_is_cancelled_and_collected(gpu_engine):
+    """A ticket dropped without wait() (a caller that gave up): its finaliser cancels the search
+    and collects it, so the job leaves the pool and its cancel word is no longer read."""
+    import gc
+    tok = _lib.CancelToken()
+    t = gpu_engine.submit(bytes(range(40, 72)), M64, device_mask=1, cancel=tok)
+    assert t.wait(0.05) is None
+    assert gpu_engine.pool_status()[1] >= 1
+    del t, tok
+    gc.collect()
+    deadline = time.time() + 5
+    while gpu_engine.pool_status() != (0, 0) and time.time() < deadline:
+        time.sleep(0.01)
+    assert gpu_engine.pool_status() == (0, 0)
+    r = gpu_engine.submit(bytes(range(72, 104)), RECEIVE, device_mask=1).wait(30)  # the pool still serves
+    assert r.status == _lib.NPOW_OK
