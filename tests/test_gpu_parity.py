@@ -164,6 +164,26 @@ def test_search_cancel_from_another_thread(gpu_engine):
     assert time.time() - t0 < 5
 
 
+def test_blocking_search_releases_the_gil(gpu_engine):
+    """npow_search blocks its caller's thread inside the library with the GIL released
+    (ctypes.CDLL): Python code in other threads keeps running at full speed meanwhile."""
+    def spin(seconds):
+        n, end = 0, time.perf_counter() + seconds
+        while time.perf_counter() < end:
+            n += 1
+        return n
+    alone = spin(0.2)
+    tok = _lib.CancelToken()
+    th = threading.Thread(target=lambda: gpu_engine.search(bytes(range(9, 41)), M64, cancel=tok))
+    th.start()
+    time.sleep(0.05)
+    beside = spin(0.2)
+    tok.set()
+    th.join(10)
+    assert not th.is_alive()
+    assert beside > 0.5 * alone, (beside, alone)
+
+
 def test_device_masks(gpu_engine):
     root = bytes(range(1, 33))
     n = gpu_engine.n_devices
