@@ -179,7 +179,7 @@ int check_init() {
 int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t start, uint64_t count,
                  const volatile uint32_t* cancel, std::vector<uint64_t>& hits, uint64_t& n_total,
                  bool& cancelled) {
-  std::lock_guard<std::mutex> lk(d.mu);
+  TaskLock lk(d);
   HIPTRY(hipSetDevice(d.hip_id));
   int rc = reset_task(d);
   if (rc) return rc;
@@ -514,7 +514,7 @@ int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t cou
   if (device < 0 || device >= (int)g_devs.size() || !root || (count && !values_out))
     return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
   Device& d = *g_devs[device];
-  std::lock_guard<std::mutex> lk(d.mu);
+  TaskLock lk(d);
   HIPTRY(hipSetDevice(d.hip_id));
   int rc = reset_task(d);
   if (rc) return rc;
@@ -541,7 +541,7 @@ int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, 
     return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
   if (n == 0) return NPOW_OK;
   Device& d = *g_devs[device];
-  std::lock_guard<std::mutex> lk(d.mu);
+  TaskLock lk(d);
   HIPTRY(hipSetDevice(d.hip_id));
   std::vector<uint64_t> words((size_t)n * 4);
   for (uint32_t i = 0; i < n; ++i)

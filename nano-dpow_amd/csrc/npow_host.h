@@ -41,6 +41,7 @@ struct Device {
   hipEvent_t ev_start[kEventRing] = {};
   hipEvent_t ev_stop[kEventRing] = {};
   std::mutex mu;                 // one task (sweep / values / pool work) per device at a time
+  std::atomic<int> tasks_waiting{0};  // sweep / values calls waiting for `mu` (TaskLock)
   // work pool (npow_pool.cpp)
   PoolDevState* pst = nullptr;         // device memory
   PoolMailbox* pmb = nullptr;          // pinned host (coherent), host view
@@ -80,6 +81,28 @@ inline void cpu_relax() {
   __builtin_ia32_pause();
 #endif
 }
+
+// A sweep / values call takes the device from the work pool: it announces itself, the pool
+// worker stops launching, lets its in-flight launches end (on their budget or a win) and
+// releases `mu`; the worker resumes once the call has finished.  Without the announcement a
+// device kept busy by a stream of searches would never be free for the call.
+class TaskLock {
+ public:
+  explicit TaskLock(Device& d) : d_(d), lk_(d.mu, std::defer_lock) {
+    d_.tasks_waiting.fetch_add(1);
+    try {
+      lk_.lock();
+    } catch (...) {
+      d_.tasks_waiting.fetch_sub(1);
+      throw;
+    }
+    d_.tasks_waiting.fetch_sub(1);
+  }
+
+ private:
+  Device& d_;
+  std::unique_lock<std::mutex> lk_;
+};
 
 // Devices selected by a mask (0 = all), excluding dead ones.
 std::vector<Device*> select_devices(uint64_t mask);

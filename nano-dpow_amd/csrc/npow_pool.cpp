@@ -466,7 +466,8 @@ int Worker::step() {
   adopt();
   check_slots();
   if (int rc = queue_readbacks()) return rc;  // before the next launch: it no longer holds them
-  if (int rc = launch()) return rc;
+  if (d_.tasks_waiting.load() == 0)            // a sweep / values call is waiting: drain instead
+    if (int rc = launch()) return rc;
   if (int rc = retire()) return rc;
   return NPOW_OK;
 }
@@ -495,6 +496,14 @@ void Worker::run() {
       std::unique_lock<std::mutex> lk(g_pool.mu);
       g_pool.cv_work.wait(lk, [&] { return !g_pool.running || wants_device_locked(d_.id); });
       if (!g_pool.running) return;
+      continue;
+    }
+    if (d_.tasks_waiting.load() > 0 && q_.empty()) {
+      // hand the device to a waiting sweep / values call (TaskLock); lock() below then waits
+      // for it to finish
+      if (dev_lock_.owns_lock()) dev_lock_.unlock();
+      while (d_.tasks_waiting.load() > 0 && !g_exiting.load(std::memory_order_relaxed))
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
       continue;
     }
     if (!dev_lock_.owns_lock()) dev_lock_.lock();  // waits behind a sweep / values task on this device

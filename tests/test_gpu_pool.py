@@ -234,3 +234,26 @@ def test_abandoned_ticket_is_cancelled_and_collected(gpu_engine):
     assert gpu_engine.pool_status() == (0, 0)
     r = gpu_engine.submit(bytes(range(72, 104)), RECEIVE, device_mask=1).wait(30)  # the pool still serves
     assert r.status == _lib.NPOW_OK
+
+
+def test_sweep_and_values_are_not_starved_by_endless_searches(gpu_engine):
+    """Searches that never end keep the pool worker busy; a sweep and a values call still get
+    the device (the worker drains its launches and hands it over) and the searches resume."""
+    toks = [_lib.CancelToken() for _ in range(6)]
+    ts = [gpu_engine.submit(r, M64, device_mask=1, cancel=c) for r, c in zip(_roots(19, 6), toks)]
+    time.sleep(0.1)
+    root = bytes(range(11, 43))
+    t0 = time.perf_counter()
+    hits = gpu_engine.sweep(root, 0xfff0000000000000, 0, 1 << 22, device_mask=1)
+    vals = gpu_engine.values(root, 0, 4096)
+    dt = time.perf_counter() - t0
+    assert hits == oracle.sweep(root, 0xfff0000000000000, 0, 1 << 22)
+    assert vals == oracle.work_values([root] * 4096, list(range(4096)))
+    assert dt < 2.0, dt
+    gpu_engine.reset_stats(0)
+    time.sleep(0.1)
+    assert gpu_engine.stats(0).launches > 0  # the searches are running again
+    for c in toks:
+        c.set()
+    for t in ts:
+        assert t.wait(30).status == _lib.NPOW_CANCELLED
