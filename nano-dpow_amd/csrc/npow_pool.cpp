@@ -42,7 +42,13 @@ namespace {
 
 constexpr int kPending = 100;  // job status before it is decided
 constexpr double kYieldMinUs = 1500.0;  // yield a running launch only if more budget than this is left
+constexpr int kIdleSpinUs = 2000;       // an idle worker polls for new jobs this long before sleeping
+constexpr double kPrelaunchUs = 2000.0;  // queue the next launch when the running one has this much budget left
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
+const bool g_trace_lat = getenv("NANOPOW_TRACE_LATENCY") != nullptr;
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
 #define NPOW_DBG(...)                     \
   do {                                    \
     if (g_debug) fprintf(stderr, __VA_ARGS__); \
@@ -72,6 +78,8 @@ struct Job {
   std::atomic<bool> cancel_req{false};
 
   bool cancel_seen() const { return cancel_req.load(std::memory_order_relaxed) || (cancel && load_acquire(cancel)); }
+  // NANOPOW_TRACE_LATENCY: host timestamps of the job's life (steady clock, us), printed by pool_wait
+  double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0;
 };
 using JobP = std::shared_ptr<Job>;
 
@@ -123,6 +131,7 @@ void finish_locked(const JobP& j) {
     else j->status = NPOW_EXHAUSTED;
     j->decided = true;
   }
+  if (g_trace_lat) j->t_finish = now_us();
   j->finished = true;
   auto it = std::find(g_pool.active.begin(), g_pool.active.end(), j);
   if (it != g_pool.active.end()) g_pool.active.erase(it);
@@ -237,6 +246,7 @@ void Worker::adopt() {
     sl.win_seen = sl.requeue = sl.no_more = sl.readback = false;
     sl.fresh = true;
     j->on_dev[k] = 1;
+    if (g_trace_lat && j->t_adopt == 0) j->t_adopt = now_us();
     if (!j->seen_dev[k]) adopted = true;  // a new job: worth ending a long launch for
     j->seen_dev[k] = 1;
   }
@@ -278,6 +288,7 @@ void Worker::handle_win(int s) {
   const uint64_t v = __atomic_load_n(&pw.value, __ATOMIC_RELAXED);
   const uint64_t cpu_v = host_work_value(j.pre.m, n);
   std::lock_guard<std::mutex> g(g_pool.mu);
+  if (g_trace_lat && j.t_win == 0) j.t_win = now_us();
   if (cpu_v == v && v >= j.threshold) {
     j.invalid_streak[sl.k] = 0;
     decide_locked(j, NPOW_OK, n, v);
@@ -328,6 +339,13 @@ void Worker::check_slots() {
 
 int Worker::launch() {
   if (q_.size() >= 2) return NPOW_OK;
+  // The second launch in flight only has to be queued before the running one ends (its budget
+  // is known): queued early, it would sit behind a launch that a win ends, and the job could
+  // only be retired after it too had started and drained (~20 us of every search's latency).
+  if (q_.size() == 1 && g_budget_us.load() > 0 &&
+      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - front_start_).count() <
+          (double)g_budget_us.load() - kPrelaunchUs)
+    return NPOW_OK;
   const uint32_t iters = g_iters.load();
   const uint32_t W = (uint32_t)pool_grid_of(d_) * (kBlock / 64);
   PoolTable& t = *d_.h_tab[ring_];
@@ -365,6 +383,7 @@ int Worker::launch() {
         pe.bounded = 0;
       }
       issued += pe.count;
+      if (g_trace_lat && j.t_launch == 0) j.t_launch = now_us();
       if (j.max_per_dev && issued >= j.max_per_dev) sl.no_more = true;
       sl.fresh = false;
     }
@@ -408,6 +427,10 @@ int Worker::retire() {
     if (e == hipErrorNotReady) break;
     if (e != hipSuccess) return fail(NPOW_ERR_HIP, std::string("pool launch: ") + hipGetErrorString(e));
     account_launch(d_, q_.front().ring);
+    if (g_trace_lat)
+      for (Slot& sl : slots_)
+        if (sl.state == SlotState::kDraining && sl.job && sl.job->t_win != 0 && sl.job->t_kend == 0)
+          sl.job->t_kend = now_us();
     NPOW_DBG("nanopow[%d]: launch %llu done\n", d_.id, (unsigned long long)q_.front().seq);
     q_.pop_front();
     front_start_ = std::chrono::steady_clock::now();  // the next one (if any) has just started
@@ -493,6 +516,15 @@ void Worker::run() {
     if (!busy()) adopt();  // jobs admitted since the last look
     if (!busy()) {
       if (dev_lock_.owns_lock()) dev_lock_.unlock();
+      // Spin a little before sleeping: a serial client submits its next request a few tens of
+      // microseconds after the last one ends, and a condition-variable wake-up costs about as
+      // much as the search itself at receive difficulty.
+      const auto spin_end = std::chrono::steady_clock::now() + std::chrono::microseconds(kIdleSpinUs);
+      while (g_pool.version.load(std::memory_order_acquire) == seen_version_ &&
+             !g_exiting.load(std::memory_order_relaxed) && d_.tasks_waiting.load() == 0 &&
+             std::chrono::steady_clock::now() < spin_end)
+        cpu_relax();
+      if (g_pool.version.load(std::memory_order_acquire) != seen_version_) continue;
       std::unique_lock<std::mutex> lk(g_pool.mu);
       g_pool.cv_work.wait(lk, [&] { return !g_pool.running || wants_device_locked(d_.id); });
       if (!g_pool.running) return;
@@ -624,6 +656,7 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   j->dev_done.assign(G, 0);
   j->invalid_streak.assign(G, 0);
   j->pending_devs = (int)G;
+  if (g_trace_lat) j->t_submit = now_us();
   std::lock_guard<std::mutex> g(g_pool.mu);
   if (!g_pool.running) return fail(NPOW_ERR_NOT_INITIALISED, "engine is shut down");
   j->ticket = g_pool.next_ticket++;
@@ -656,6 +689,10 @@ int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* va
     g_pool.cv_done.wait_until(lk, wake);
   }
   if (nonces_done) *nonces_done = j->done;
+  if (g_trace_lat)
+    fprintf(stderr, "nanopow-lat adopt %.1f launch %.1f win %.1f kend %.1f finish %.1f return %.1f\n",
+            j->t_adopt - j->t_submit, j->t_launch - j->t_submit, j->t_win - j->t_submit, j->t_kend - j->t_submit,
+            j->t_finish - j->t_submit, now_us() - j->t_submit);
   const int st = j->status;
   g_pool.tickets.erase(ticket);
   if (st == NPOW_OK) {
