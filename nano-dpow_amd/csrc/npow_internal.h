@@ -115,6 +115,16 @@ struct PoolTable {
 };
 inline size_t pool_table_bytes(uint32_t n) { return offsetof(PoolTable, e) + (size_t)n * sizeof(PoolEntry); }
 
+// The same table with at most kArgEntries entries, passed by value as the launch's kernel
+// arguments (npow_pool_kernel_arg): its bytes are a prefix of PoolTable's.
+constexpr int kArgEntries = 16;
+struct PoolTableArg {
+  uint8_t header[offsetof(PoolTable, e)];
+  PoolEntry e[kArgEntries];
+};
+static_assert(offsetof(PoolTableArg, e) == offsetof(PoolTable, e), "PoolTableArg must be a prefix of PoolTable");
+static_assert(sizeof(PoolTableArg) + 2 * sizeof(void*) <= 4096, "kernel arguments are limited to 4 KiB");
+
 struct PoolSlotWord {
   unsigned long long dead;  // highest generation known dead in this slot
   uint8_t pad[56];
@@ -144,6 +154,9 @@ hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs
 // bounded: the table holds a bounded entry (selects the kernel variant with per-lane range tests)
 hipError_t launch_pool(int grid, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
                        PoolMailbox* mb);
+// The same with the table (n <= kArgEntries) passed in the kernel arguments: no upload.
+hipError_t launch_pool_arg(int grid, hipStream_t stream, const PoolTable& host_tab, bool bounded, PoolDevState* st,
+                           PoolMailbox* mb);
 // Fill a.u[] for one root (host).
 inline void fill_uniforms(LaunchArgs& a, const RootPrecomp& pre) { npow_asm_uniforms(pre.m, a.u); }
 

@@ -29,6 +29,7 @@
 //    the host sorts).  Values mode: grid-stride, writes every value (parity tests).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <string.h>
 
 #include "npow_internal.h"
 
@@ -277,19 +278,13 @@ __device__ __forceinline__ uint64_t load_dead(PoolDevState* st, uint32_t slot) {
 #define NPOW_POOL_NUM_SGPR 0
 #endif
 template <bool BOUNDED>
-__global__ __launch_bounds__(kBlock)
-#if NPOW_POOL_NUM_SGPR
-__attribute__((amdgpu_num_sgpr(NPOW_POOL_NUM_SGPR)))
-#endif
-void npow_pool_kernel(const PoolTable* __restrict__ tab,
-                                                           PoolDevState* __restrict__ st,
-                                                           PoolMailbox* __restrict__ mb) {
-  uint64_t t_start;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
+__device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
+                                          PoolMailbox* __restrict__ mb, const uint64_t t_start) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t w = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
   const uint32_t W = gridDim.x * (kBlock / 64);
   const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask, budget = tab->budget;
+  const uint64_t yield_base = tab->yield_base;  // read once: the loop below compares against it
   unsigned long long* const done_base = &st->done[0][(blockIdx.x % kPoolDoneShards) * 8];
   // Time budget.  VALU issue on a SIMD goes to its OLDEST wave first (MI355X_MICROARCH.md:
   // priority, then age), so the 8 waves of a SIMD do not progress together: the oldest runs
@@ -315,7 +310,7 @@ void npow_pool_kernel(const PoolTable* __restrict__ tab,
 #define NPOW_POOL_POLL 3
 #endif
       const uint64_t dead = (NPOW_POOL_POLL & 1) ? load_dead(st, c.slot) : 0;
-      uint64_t kill = 0, yld = tab->yield_base;
+      uint64_t kill = 0, yld = yield_base;
       if ((NPOW_POOL_POLL & 2) && ((it + w) & poll_mask) == 0) {
         kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         yld = __hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -348,7 +343,7 @@ void npow_pool_kernel(const PoolTable* __restrict__ tab,
         }
         break;
       }
-      if (__builtin_expect(readlane64(yld, 0) != tab->yield_base, 0)) {
+      if (__builtin_expect(readlane64(yld, 0) != yield_base, 0)) {
         // the host has new jobs for this device: end every unbounded entry of this launch
         // (their jobs come back in the next launch's table with new generations)
         if (lane == 0)
@@ -396,12 +391,54 @@ void npow_pool_kernel(const PoolTable* __restrict__ tab,
 #endif
 }
 
+// The table in device memory (uploaded in stream order before the launch).
+template <bool BOUNDED>
+__global__ __launch_bounds__(kBlock)
+#if NPOW_POOL_NUM_SGPR
+__attribute__((amdgpu_num_sgpr(NPOW_POOL_NUM_SGPR)))
+#endif
+void npow_pool_kernel(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
+                      PoolMailbox* __restrict__ mb) {
+  uint64_t t_start;  // first instruction: see pool_body
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
+  pool_body<BOUNDED>(tab, st, mb, t_start);
+}
+
+// Up to kArgEntries entries: the table travels in the launch's kernel arguments, so no copy
+// has to run on the stream before the kernel (a blit dispatch, several microseconds of every
+// search's latency).  The body reads it in place through the kernarg segment pointer (taking
+// the address of a by-value parameter would copy it to scratch).
+template <bool BOUNDED>
+__global__ __launch_bounds__(kBlock)
+#if NPOW_POOL_NUM_SGPR
+__attribute__((amdgpu_num_sgpr(NPOW_POOL_NUM_SGPR)))
+#endif
+void npow_pool_kernel_arg(const PoolTableArg targ, PoolDevState* __restrict__ st, PoolMailbox* __restrict__ mb) {
+  uint64_t t_start;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
+  (void)targ;
+  const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();  // address space 4 -> generic
+  pool_body<BOUNDED>(tab, st, mb, t_start);
+}
+
 hipError_t launch_pool(int grid, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
                        PoolMailbox* mb) {
   if (bounded)
     npow_pool_kernel<true><<<grid, kBlock, 0, stream>>>(tab, st, mb);
   else
     npow_pool_kernel<false><<<grid, kBlock, 0, stream>>>(tab, st, mb);
+  return hipGetLastError();
+}
+
+hipError_t launch_pool_arg(int grid, hipStream_t stream, const PoolTable& host_tab, bool bounded, PoolDevState* st,
+                           PoolMailbox* mb) {
+  if (host_tab.n > (uint32_t)kArgEntries) return hipErrorInvalidValue;
+  PoolTableArg a;
+  memcpy(&a, &host_tab, pool_table_bytes(host_tab.n));
+  if (bounded)
+    npow_pool_kernel_arg<true><<<grid, kBlock, 0, stream>>>(a, st, mb);
+  else
+    npow_pool_kernel_arg<false><<<grid, kBlock, 0, stream>>>(a, st, mb);
   return hipGetLastError();
 }
 

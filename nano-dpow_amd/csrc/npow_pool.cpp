@@ -394,9 +394,15 @@ int Worker::launch() {
   // The table goes up in stream order right before its launch.  (Uploading it on a second
   // stream beside the running launch, joined by an event, cost 1.5-2 % of kernel throughput:
   // the copy is a blit kernel that competes with the running launch.)
-  HIPTRY(hipMemcpyAsync(d_.d_tab[r], d_.h_tab[r], bytes, hipMemcpyHostToDevice, d_.stream));
-  HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
-  HIPTRY(launch_pool(pool_grid_of(d_), d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
+  static const bool force_upload = getenv("NANOPOW_TABLE_UPLOAD") != nullptr;  // A/B switch
+  if (n <= (uint32_t)kArgEntries && !force_upload) {  // the table rides in the kernel arguments
+    HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
+    HIPTRY(launch_pool_arg(pool_grid_of(d_), d_.stream, t, bounded, d_.pst, d_.pmb_dev));
+  } else {
+    HIPTRY(hipMemcpyAsync(d_.d_tab[r], d_.h_tab[r], bytes, hipMemcpyHostToDevice, d_.stream));
+    HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
+    HIPTRY(launch_pool(pool_grid_of(d_), d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
+  }
   HIPTRY(hipEventRecord(d_.ev_stop[r], d_.stream));
   if (q_.empty()) front_start_ = std::chrono::steady_clock::now();
   NPOW_DBG("nanopow[%d]: launch %llu n=%u slots:", d_.id, (unsigned long long)seq_, n);
