@@ -15,7 +15,8 @@
 // its waves move on to the other live roots (npow_kernel.hip, npow_pool_kernel).
 //
 // Threads: one persistent worker per device (started by npow_init) owns the device's
-// stream, its slot table and two launches in flight; callers block in pool_wait.  The
+// stream, its slot table and up to two launches in flight (the second is queued only near
+// the end of the first one's budget); callers block in pool_wait.  The
 // only cross-device datum is a job's outcome: the first device whose winner passes CPU
 // re-validation decides the job, the others raise their slot's kill word (pinned host
 // memory that the waves poll) and retire it.  No collective, no device-to-device traffic.
