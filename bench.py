@@ -59,9 +59,15 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 WORLD = int(os.environ.get("WORLD_SIZE", "1"))
 LOCAL_RANK = int(os.environ.get("LOCAL_RANK", "0"))
-if WORLD > 1 and "HIP_VISIBLE_DEVICES" not in os.environ:
-    # one GPU per rank: the engine of rank r sees only GPU LOCAL_RANK (as device 0)
-    os.environ["HIP_VISIBLE_DEVICES"] = str(LOCAL_RANK)
+if WORLD > 1:
+    # one GPU per rank: the engine of rank r sees only GPU LOCAL_RANK (as device 0).  A launcher
+    # that already exported a device list keeps its list; the rank takes its LOCAL_RANK-th entry.
+    _vis = os.environ.get("HIP_VISIBLE_DEVICES")
+    if _vis is None:
+        os.environ["HIP_VISIBLE_DEVICES"] = str(LOCAL_RANK)
+    elif "," in _vis:
+        _ids = [x for x in _vis.split(",") if x.strip()]
+        os.environ["HIP_VISIBLE_DEVICES"] = _ids[LOCAL_RANK % len(_ids)]
 sys.path.insert(0, os.path.join(HERE, "nano-dpow_amd"))
 
 SEND = 0xfffffff800000000
@@ -701,7 +707,9 @@ def main() -> int:
         eng.set_tuning(args.iters, 0, 0)
     if args.budget_us >= 0 or args.pool_blocks:
         eng.set_pool_tuning(None if args.budget_us < 0 else args.budget_us, args.pool_blocks)
-    dev = 0
+    # normally 0 (the rank's only visible GPU); if the runtime still shows several (a device list
+    # exported under another variable), the rank takes the LOCAL_RANK-th so ranks never share a GPU
+    dev = LOCAL_RANK % eng.n_devices if WORLD > 1 else 0
     if args.workload != "search":
         fn = {"allgpus": workload_allgpus, "sweep": workload_sweep, "burst": workload_burst,
               "sustained": workload_sustained, "dpow": workload_dpow, "receive": workload_receive}[args.workload]

@@ -5,7 +5,7 @@ set -o pipefail
 TAG=${1:-r01}
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 900 python3 -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu_$TAG.log 2>&1 &&
+timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu_$TAG.log 2>&1 &&
 timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 &&
 timeout -k 10 400 python3 bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err &&
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- python3 bench.py --no-cpu-baseline --steps 200 > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/prof_$TAG.err
