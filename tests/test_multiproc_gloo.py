@@ -77,3 +77,18 @@ def test_device_strides_disjoint():
         assert len(set(starts)) == G
         if G > 1:
             assert all(b - a >= (1 << 64) // G for a, b in zip(starts, starts[1:]))
+
+
+@pytest.mark.parametrize("preset,local_rank,want", [(None, 3, "3"), ("0,1,2,3,4,5,6,7", 5, "5"),
+                                                    ("4,6", 1, "6"), ("2", 0, "2")])
+def test_bench_rank_sees_only_its_gpu(preset, local_rank, want):
+    """Under torchrun each bench.py rank must see exactly one GPU: LOCAL_RANK, or the LOCAL_RANK-th
+    entry of a device list the launcher already exported (else every rank would search on GPU 0)."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k != "HIP_VISIBLE_DEVICES"}
+    env.update(WORLD_SIZE="8", LOCAL_RANK=str(local_rank), RANK=str(local_rank))
+    if preset is not None:
+        env["HIP_VISIBLE_DEVICES"] = preset
+    out = subprocess.run([sys.executable, "-c", "import os, bench; print(os.environ['HIP_VISIBLE_DEVICES'])"],
+                         cwd=ROOT, env=env, capture_output=True, text=True, timeout=120, check=True)
+    assert out.stdout.strip() == want
