@@ -167,7 +167,23 @@ def gen_sweep36() -> None:
                              "method": f"c-oracle exhaustive on {os.cpu_count()} threads ({dt:.0f} s), every hit re-hashed by hashlib"})
 
 
+def gen_sweep30() -> None:
+    """the sweep root's [0, 2^30) scanned by hashlib alone (no C oracle in
+    the loop) at fffff000 (~1,024 hits); its fffffff8 subset must equal the 2^36 fixture's prefix."""
+    t0 = time.time()
+    root, count = SWEEP_ROOT, 1 << 30
+    hl = hashlib_sweep(root, LOW, 0, count, procs=os.cpu_count() or 8)
+    co = oracle.sweep(root, LOW, 0, count)
+    assert hl == co, "C oracle disagrees with hashlib"
+    dt = time.time() - t0
+    dump("sweep_2p30_hashlib.json", {"generator": "tests/golden/gen_golden.py sweep30",
+                                     "root": root.hex(), "threshold": f"{LOW:016x}", "start": "0000000000000000",
+                                     "count": count, "hits": [f"{n:016x}" for n in hl],
+                                     "method": f"hashlib exhaustive on {os.cpu_count()} processes ({dt:.0f} s); "
+                                               "C oracle agrees"})
+
+
 if __name__ == "__main__":
     what = sys.argv[1:] or ["values", "kat", "sweeps"]
     for w in what:
-        {"values": gen_values, "kat": gen_kat, "sweeps": gen_sweeps, "sweep36": gen_sweep36}[w]()
+        {"values": gen_values, "kat": gen_kat, "sweeps": gen_sweeps, "sweep36": gen_sweep36, "sweep30": gen_sweep30}[w]()

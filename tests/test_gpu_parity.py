@@ -58,6 +58,13 @@ def test_sweep_fixtures(gpu_engine):
         assert [f"{h:016x}" for h in got] == c["hits"], c["method"]
 
 
+def test_sweep_2p30_hashlib_fixture(gpu_engine):
+    """[0, 2^30) of the config-3 root at fffff000: ~1,024 hits, fixture from hashlib alone."""
+    g = load_golden("sweep_2p30_hashlib.json")
+    got = gpu_engine.sweep(bytes.fromhex(g["root"]), int(g["threshold"], 16), 0, g["count"], cap=1 << 12)
+    assert [f"{h:016x}" for h in got] == g["hits"]
+
+
 def test_sweep_2p36_full_size(gpu_engine):
     """BASELINE config 3: exhaustive 2^36 sweep, bit-exact hit set vs the CPU fixture."""
     path = os.path.join(os.path.dirname(__file__), "golden", "sweep_2p36.json")

@@ -91,3 +91,17 @@ def test_sweep_2p36_fixture_if_present():
     assert hits == sorted(hits)
     for n in hits:
         assert oracle.work_value_hashlib(root, n) >= thr
+
+
+def test_sweep_2p36_prefix_pinned_by_hashlib_2p30():
+    """The 2^36 fixture (C oracle) below 2^30 equals the fffffff8 subset of a hashlib-only
+    exhaustive scan of [0, 2^30) at fffff000."""
+    g36 = load_golden("sweep_2p36.json")
+    g30 = load_golden("sweep_2p30_hashlib.json")
+    assert g30["root"] == g36["root"] and g30["start"] == "0000000000000000" and g30["count"] == 1 << 30
+    root, send, low = bytes.fromhex(g30["root"]), int(g36["threshold"], 16), int(g30["threshold"], 16)
+    hits30 = [int(h, 16) for h in g30["hits"]]
+    assert 900 < len(hits30) < 1150 and hits30 == sorted(hits30)  # Poisson(1024)
+    vals = {n: oracle.work_value_hashlib(root, n) for n in hits30}
+    assert all(v >= low for v in vals.values())
+    assert [n for n in hits30 if vals[n] >= send] == [int(h, 16) for h in g36["hits"] if int(h, 16) < 1 << 30]
