@@ -125,28 +125,78 @@ def cpu_baseline(seconds: float = 12.0):
             "hashlib_1core_gnps": round(hl / 1e9, 6)}
 
 
-def run_timed(search, stats, reset_stats, steps: int, warmup: int, rank: int, world: int, dist=None):
-    """Warm up, then time exactly `steps` searches bracketed by barriers; reduce over ranks.
+class NodeQueue:
+    """The timed searches of a multi-rank run as ONE node-wide queue: a counter in a file that every
+    rank of this node draws from under flock (~10 us a draw).  A first-win search hashes a random
+    number of nonces (exponential, coefficient of variation 1), so K fixed roots per rank would leave
+    the ranks with the luckier roots idle at the closing barrier -- with K = 300 the slowest of 8
+    ranks runs ~8 % past the mean.  Drawing from one queue, as a DPoW node's GPUs serve one request
+    stream, every GPU stays busy until the N*K searches are done; ranks finish within about one
+    search of each other."""
 
-    search(i) -> (seconds, nonces_hashed); stats() -> (kernel_ms, kernel_nonces, launches).
-    Returns the rank-0 view: (total_nonces, max_wall_s, all_ttw_s, kernel_ms, kernel_nonces, launches)
-    with kernel_* summed over ranks."""
+    def __init__(self, dist, rank: int, total: int):
+        import tempfile
+        box = [None]
+        if rank == 0:
+            fd, path = tempfile.mkstemp(prefix="nanopow_bench_queue_")
+            os.write(fd, (0).to_bytes(8, "little"))
+            os.close(fd)
+            box = [path]
+        dist.broadcast_object_list(box, src=0)
+        self.path, self.total, self.rank = box[0], total, rank
+        self.fd = os.open(self.path, os.O_RDWR)
+
+    def draw(self):
+        import fcntl
+        fcntl.flock(self.fd, fcntl.LOCK_EX)
+        try:
+            i = int.from_bytes(os.pread(self.fd, 8, 0), "little")
+            if i < self.total:
+                os.pwrite(self.fd, (i + 1).to_bytes(8, "little"), 0)
+        finally:
+            fcntl.flock(self.fd, fcntl.LOCK_UN)
+        return i if i < self.total else None
+
+    def close(self):
+        os.close(self.fd)
+        if self.rank == 0:
+            os.unlink(self.path)
+
+
+def run_timed(search, stats, reset_stats, steps: int, warmup: int, rank: int, world: int, dist=None):
+    """Warm up, then time exactly `steps` searches per rank bracketed by barriers; reduce over ranks.
+
+    With several ranks on one node the world * steps timed searches come from one NodeQueue (search
+    i of the job is root R_{1,000,000 + i} whichever rank draws it); a rank alone searches R_{1,000,000
+    + s}, s < steps.  search(i) -> (seconds, nonces_hashed); stats() -> (kernel_ms, kernel_nonces,
+    launches).  Returns the rank-0 view: (total_nonces, max_wall_s, all_ttw_s, kernel_ms,
+    kernel_nonces, launches) with kernel_* summed over ranks."""
     base_idx = 1_000_000 * (rank + 1)
     for w in range(warmup):
         search(base_idx + 900_000 + w)
     reset_stats()
+    one_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
+    queue = NodeQueue(dist, rank, world * steps) if (dist is not None and world > 1 and one_node) else None
     if dist is not None:
         dist.barrier()
     # npow_search returns only after its streams drained, so the GPU is idle at both barriers
     t0 = time.perf_counter()
     ttw, nonces = [], 0
-    for s in range(steps):
-        dt, n = search(base_idx + s)
-        ttw.append(dt)
-        nonces += n
+    if queue is None:
+        for s in range(steps):
+            dt, n = search(base_idx + s)
+            ttw.append(dt)
+            nonces += n
+    else:
+        while (i := queue.draw()) is not None:
+            dt, n = search(1_000_000 + i)
+            ttw.append(dt)
+            nonces += n
     if dist is not None:
         dist.barrier()
     wall = time.perf_counter() - t0
+    if queue is not None:
+        queue.close()
     kern_ms, kern_nonces, launches = stats()
     if dist is None:
         return nonces, wall, ttw, kern_ms, kern_nonces, launches
@@ -195,7 +245,10 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
                         "fffffff800000000, first-win search, p50/p99 time-to-work",
             "threshold": "fffffff800000000",
             "searches_per_gpu": steps,
-            "parallelism": f"dp{world} (disjoint roots per GPU, no collective)",
+            "searches_total": len(all_ttw),
+            "parallelism": f"dp{world} (disjoint roots per GPU, no collective)" if world == 1 else
+                           f"dp{world} ({len(all_ttw)} searches drawn from one node-wide queue by {world} "
+                           "one-GPU ranks; disjoint roots, no collective)",
         },
         "p50_ttw_ms": round(pct(all_ttw, 50) * 1e3, 3),
         "p99_ttw_ms": round(pct(all_ttw, 99) * 1e3, 3),

@@ -30,8 +30,11 @@ def _worker(rank, world, port, q):
     import oracle
     dist.init_process_group("gloo", rank=rank, world_size=world)
 
+    drawn = []
+
     def search(i):
         import time
+        drawn.append(i)
         t = time.perf_counter()
         scanned, nonce = oracle.search(bench.bench_root(i), 0xffff000000000000, bench.bench_start(i), 1 << 22)
         assert nonce is not None
@@ -40,7 +43,7 @@ def _worker(rank, world, port, q):
     res = bench.run_timed(search, lambda: (10.0 * (rank + 1), 1000 * (rank + 1), 2), lambda: None,
                           steps=5, warmup=1, rank=rank, world=world, dist=dist)
     line = bench.result_line(world, 5, 1, *res)
-    q.put((rank, res, line))
+    q.put((rank, res, line, drawn[1:]))  # drawn[0] is the rank's warmup search
     dist.barrier()
     dist.destroy_process_group()
 
@@ -52,10 +55,11 @@ def test_two_rank_gloo_bench_reduction():
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
     for p in procs:
         p.start()
-    out = {}
+    out, timed = {}, []
     for _ in range(2):
-        r, res, line = q.get(timeout=120)
+        r, res, line, drawn = q.get(timeout=120)
         out[r] = (res, line)
+        timed.extend(drawn)
     for p in procs:
         p.join(60)
         assert p.exitcode == 0
@@ -63,6 +67,9 @@ def test_two_rank_gloo_bench_reduction():
     (n1, w1, ttw1, km1, kn1, l1), _ = out[1]
     assert n0 == n1 and w0 == w1          # every rank holds the reduced values
     assert len(ttw0) == 10                # gathered from both ranks
+    # the 2 x 5 timed searches came from one node-wide queue: every job root exactly once
+    assert sorted(timed) == [1_000_000 + i for i in range(10)]
+    assert line0["config"]["searches_total"] == 10
     assert km0 == 30.0 and kn0 == 3000 and l0 == 4
     assert line0["n_gpus"] == 2 and line0["scaling"] == "weak"
     assert line0["value"] == round(n0 / w0 / 1e9, 4)
