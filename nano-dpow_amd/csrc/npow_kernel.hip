@@ -309,9 +309,13 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
 #ifndef NPOW_POOL_POLL
 #define NPOW_POOL_POLL 3
 #endif
+      // Only the hash, the nonce, the threshold compare and the dead compare are VALU work on
+      // the common path: the host words are loaded and compared only by polling waves, and the
+      // clock compare is scalar (a default value or a 64-bit compare here costs VALU issue).
       const uint64_t dead = (NPOW_POOL_POLL & 1) ? load_dead(st, c.slot) : 0;
-      uint64_t kill = 0, yld = yield_base;
-      if ((NPOW_POOL_POLL & 2) && ((it + w) & poll_mask) == 0) {
+      const bool poll = (NPOW_POOL_POLL & 2) && ((it + w) & poll_mask) == 0;  // wave-uniform
+      uint64_t kill, yld;
+      if (__builtin_expect(poll, 0)) {
         kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         yld = __hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
@@ -343,20 +347,24 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
         }
         break;
       }
-      if (__builtin_expect(readlane64(yld, 0) != yield_base, 0)) {
-        // the host has new jobs for this device: end every unbounded entry of this launch
-        // (their jobs come back in the next launch's table with new generations)
-        if (lane == 0)
-          for (uint32_t k = 0; k < n; ++k)
-            if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
-        if (!c.bounded) break;
-      }
-      if (readlane64(kill, 0) == c.gen) {  // generations only grow: == is "this job"
-        if (lane == 0) atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen);  // relay
-        break;
+      if (__builtin_expect(poll, 0)) {
+        if (readlane64(yld, 0) != yield_base) {
+          // the host has new jobs for this device: end every unbounded entry of this launch
+          // (their jobs come back in the next launch's table with new generations)
+          if (lane == 0)
+            for (uint32_t k = 0; k < n; ++k)
+              if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
+          if (!c.bounded) break;
+        }
+        if (readlane64(kill, 0) == c.gen) {  // generations only grow: == is "this job"
+          if (lane == 0) atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen);  // relay
+          break;
+        }
       }
       if (readlane64(dead, 0) == c.gen) break;
-      if (budget && !c.bounded && now - t_start >= budget) {  // out of time: the wave is done
+      // out of time: the wave is done.  A 32-bit compare of the wrapped tick difference (s_cmp;
+      // a 64-bit one is a VALU v_cmp): exact while a launch lasts under 2^32 ticks = 42.9 s.
+      if (budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget) {
         out_of_time = true;
         break;
       }
