@@ -183,17 +183,26 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
     // sub-range (workgroups are dealt to XCDs round-robin) and then helps the others.  Claim
     // size = remaining / (2 x waves per sub-range), between 1 and max_claim (guided
     // self-scheduling, capped because a young wave is several times slower than an old one).
+    //
+    // The inner loop keeps its bookkeeping scalar: 32-bit iteration indices (a launch is at most
+    // 2^37 nonces, engine: 2^31), the per-lane range test only in the launch's last block, the
+    // host abort word loaded and tested only by polling waves, and the device stop word read as
+    // its 32-bit abort half (found is unused): besides the hash, an iteration issues the nonce
+    // add, the threshold compare and one v_readfirstlane (11 VALU instructions before).
     const uint32_t slot = a.claim_slot & 1;
     if (blockIdx.x == 0 && threadIdx.x < kClaimRanges)
       __hip_atomic_store(&st->claim[((1 - slot) * kClaimRanges + threadIdx.x) * 8], 0ull, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t T = (a.count + 63) >> 6;                                  // wave iterations
+    const uint32_t T = (uint32_t)((a.count + 63) >> 6);                      // wave iterations
+    const uint32_t last_lanes = (uint32_t)(a.count - ((uint64_t)(T - 1) << 6));  // 1..64 in block T-1
     const uint64_t W2 = 2ull * gridDim.x * (kBlock / 64) / kClaimRanges;     // 2 x waves per sub-range
+    const uint64_t lane_nonce = a.base + lane;                               // + block * 64
     const uint32_t home = blockIdx.x % kClaimRanges;
     bool go = true;
     for (uint32_t k = 0; k < kClaimRanges && go; ++k) {
       const uint32_t x = (home + k) % kClaimRanges;
-      const uint64_t lo = T * x / kClaimRanges, Tx = T * (x + 1) / kClaimRanges - lo;
+      const uint32_t lo = (uint32_t)((uint64_t)T * x / kClaimRanges);
+      const uint32_t Tx = (uint32_t)((uint64_t)T * (x + 1) / kClaimRanges) - lo;
       unsigned long long* ctr = &st->claim[(slot * kClaimRanges + x) * 8];
       uint64_t seen = 0;  // the counter as last seen by this wave
       if (k) {            // helping: start from the counter's current value (it may be nearly used up)
@@ -209,8 +218,38 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
         c = readlane64(c, 0);
         if (c >= Tx) break;
         seen = c + n;
-        const uint64_t end = seen < Tx ? seen : Tx;
-        for (uint64_t it = c; it < end && go; ++it) go = step((lo + it) << 6);
+        const uint32_t end = lo + (uint32_t)(seen < Tx ? seen : Tx);
+        for (uint32_t blk = lo + (uint32_t)c; blk < end; ++blk) {
+          // polls, issued before the hash and consumed after it (see step() above)
+          const uint32_t stop = __hip_atomic_load(&st->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          const bool poll = ((iter + wave_id) & a.poll_mask) == 0;  // wave-uniform
+          uint32_t host_abort;
+          if (__builtin_expect(poll, 0))
+            host_abort = __hip_atomic_load(&mb->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          ++iter;
+          const uint64_t nonce = lane_nonce + ((uint64_t)blk << 6);
+          const uint64_t value = npow_asm_work_value(nonce, u);
+          uint64_t hits = __ballot(value >= a.threshold);  // the compare writes the mask directly
+          if (__builtin_expect(blk == T - 1, 0)) {        // the launch's last block may be partial
+            hits &= last_lanes == 64 ? ~0ull : (1ull << last_lanes) - 1;
+            done += last_lanes;
+          } else {
+            done += 64;
+          }
+          if (__builtin_expect(hits != 0, 0) && ((hits >> lane) & 1)) {  // append every hit
+            const uint32_t hs = atomicAdd(&st->n_hits, 1u);
+            if (hs < a.cap) out[hs] = nonce;
+          }
+          if (__builtin_expect(poll, 0) && __builtin_amdgcn_readfirstlane(host_abort)) {
+            if (lane == 0) __hip_atomic_store(&st->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            go = false;
+            break;
+          }
+          if (__builtin_amdgcn_readfirstlane(stop)) {
+            go = false;
+            break;
+          }
+        }
       }
     }
   }
