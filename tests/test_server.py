@@ -249,7 +249,9 @@ def test_burst_of_concurrent_connections_is_accepted_at_once():
     def client(i):
         go.wait()
         t = time.perf_counter()
-        out[i] = post(srv.address, {"action": "work_generate", "hash": f"{i + 1:064X}", "difficulty": "ff00000000000000"},
+        # a trivial difficulty (~1 nonce per request): the latency measured is the connection's,
+        # not the oracle engine's CPU hashing under 300 threads
+        out[i] = post(srv.address, {"action": "work_generate", "hash": f"{i + 1:064X}", "difficulty": "1000000000000000"},
                       timeout=60)
         lat[i] = time.perf_counter() - t
     try:
@@ -262,5 +264,5 @@ def test_burst_of_concurrent_connections_is_accepted_at_once():
     finally:
         srv.stop()
     for i in range(n):
-        assert oracle.work_value(bytes.fromhex(f"{i + 1:064X}"), int(out[i]["work"], 16)) >= 0xff00000000000000
+        assert oracle.work_value(bytes.fromhex(f"{i + 1:064X}"), int(out[i]["work"], 16)) >= 0x1000000000000000
     assert max(lat) < 0.9, sorted(lat)[-5:]
