@@ -163,6 +163,119 @@ class NodeQueue:
             os.unlink(self.path)
 
 
+class SharedWords:
+    """32-bit words in a file every rank of this node maps (mmap, MAP_SHARED): cancel words of
+    searches that all ranks run on ONE root.  The rank whose search wins raises the word; the
+    other ranks' engines poll it as that search's cancel word (nanopow.CancelToken duck type:
+    .address / .set()) and stop within microseconds.  Every rank runs the same collectives
+    whatever happens locally (a rank without the mapping searches without a cancel word)."""
+
+    class Word:
+        def __init__(self, cw):
+            self._w = cw
+
+        @property
+        def address(self) -> int:
+            import ctypes
+            return ctypes.addressof(self._w)
+
+        def set(self) -> None:
+            self._w.value = 1
+
+        @property
+        def is_set(self) -> bool:
+            return bool(self._w.value)
+
+    def __init__(self, dist, rank: int, n: int):
+        import ctypes
+        import mmap
+        import tempfile
+        box = [None]
+        if rank == 0:
+            try:
+                fd, path = tempfile.mkstemp(prefix="nanopow_bench_cancel_")
+                os.ftruncate(fd, 4 * n)
+                os.close(fd)
+                box = [path]
+            except OSError:
+                box = [None]
+        dist.broadcast_object_list(box, src=0)
+        self.path, self.rank, self.words, self.mm, self.f = box[0], rank, None, None, None
+        if self.path is not None:
+            try:
+                self.f = open(self.path, "r+b")
+                self.mm = mmap.mmap(self.f.fileno(), 4 * n)
+                self.words = [ctypes.c_uint32.from_buffer(self.mm, 4 * i) for i in range(n)]
+            except (OSError, ValueError):
+                self.words = None
+
+    def word(self, i: int):
+        return SharedWords.Word(self.words[i]) if self.words is not None else None
+
+    def close(self) -> None:
+        # The mapping itself stays until the process exits: an engine must never poll a cancel
+        # word whose page is gone, and the mmap cannot close while ctypes words point into it.
+        self.words = None
+        if self.f is not None:
+            self.f.close()
+        if self.rank == 0 and self.path is not None:
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass
+
+
+def node_time_to_work(eng, dev: int, rank: int, world: int, dist, m: int, thr: int = SEND):
+    """One root at a time searched by ALL ranks (north_star: the nonce space split into disjoint
+    per-GPU strides, first found cancels the others): rank r scans start + r * 2^64/N; the
+    winner raises the root's shared cancel word.  Runs after the timed region; returns (rank 0)
+    {p50, p99, n, ...} of the winners' search times, or None on other ranks."""
+    spacing = (1 << 64) // world
+    words = SharedWords(dist, rank, m)
+    recs = []
+    try:
+        for i in range(m):
+            dist.barrier()
+            tok = words.word(i)
+            idx = 3_000_000 + i
+            t = time.perf_counter()
+            try:
+                r = eng.search(bench_root(idx), thr, start=(bench_start(idx) + rank * spacing) & ((1 << 64) - 1),
+                               device_mask=1 << dev, cancel=tok)
+                dt = time.perf_counter() - t
+                if r.status == 0 and tok is not None:
+                    tok.set()
+                recs.append((dt, r.status, r.nonces_done))
+            except Exception:  # keep the collectives aligned; reported as a failed search
+                recs.append((None, -1, 0))
+        dist.barrier()
+    finally:
+        words.close()
+    gathered = [None] * world
+    dist.all_gather_object(gathered, recs)
+    if rank != 0:
+        return None
+    ttw, failed, nonces = [], 0, 0
+    cancelled = sum(1 for g in gathered for rec in g if rec[1] == 1)
+    for i in range(m):
+        wins = [g[i][0] for g in gathered if g[i][1] == 0]
+        nonces += sum(g[i][2] for g in gathered)
+        if wins:
+            ttw.append(min(wins))
+        else:
+            failed += 1
+    if not ttw:
+        return {"error": "no search won", "n": m}
+    return {"p50": round(pct(ttw, 50) * 1e3, 3), "p99": round(pct(ttw, 99) * 1e3, 3),
+            "mean": round(statistics.mean(ttw) * 1e3, 3), "n": len(ttw), "failed": failed,
+            "rank_searches_cancelled": cancelled,
+            "shared_cancel": words.path is not None,
+            "nonces_per_search": round(nonces / m),
+            "note": f"one root at a time searched by all {world} ranks on disjoint strides (rank r from "
+                    "start + r*2^64/N), the first win cancelling the others through a shared-memory word; "
+                    "winner's search time at the C ABI; after the timed region, not part of value"}
+
+
 def run_timed(search, stats, reset_stats, steps: int, warmup: int, rank: int, world: int, dist=None):
     """Warm up, then time exactly `steps` searches per rank bracketed by barriers; reduce over ranks.
 
@@ -743,6 +856,8 @@ def main() -> int:
     ap.add_argument("--cpu-requests", type=int, default=4, help="receive: requests timed on the CPU reference")
     ap.add_argument("--via", choices=["abi", "http"], default="abi",
                     help="burst: submit through the C ABI work pool or POST to the HTTP work server")
+    ap.add_argument("--node-searches", type=int, default=100,
+                    help="search, N>1: roots searched by all ranks at once after the timed steps (node time-to-work)")
     ap.add_argument("--http-requests", type=int, default=100,
                     help="search, N=1: work_generate requests timed at the JSON boundary after the timed steps")
     args = ap.parse_args()
@@ -751,7 +866,9 @@ def main() -> int:
     dist = None
     if WORLD > 1:
         import torch.distributed as dist  # gloo: barrier + scalar reductions only
-        dist.init_process_group("gloo")
+        import datetime
+        # a lost rank ends the job within minutes instead of gloo's default 30
+        dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=300))
 
     import nanopow
     from nanopow import _lib
@@ -788,8 +905,13 @@ def main() -> int:
 
     res = run_timed(search, stats, lambda: eng.reset_stats(dev), args.steps, args.warmup, rank, WORLD, dist)
     http = _http_ttw(eng, args.http_requests) if (rank == 0 and WORLD == 1 and args.http_requests) else None
+    node = None
+    if dist is not None and args.node_searches > 0 and int(os.environ.get("LOCAL_WORLD_SIZE", WORLD)) == WORLD:
+        node = node_time_to_work(eng, dev, rank, WORLD, dist, args.node_searches)
     if rank == 0:
         line = result_line(WORLD, args.steps, args.warmup, *res)
+        if node:
+            line["node_ttw_ms"] = node
         if http:
             line["http_ttw_ms"] = {"p50": round(pct(http, 50) * 1e3, 3), "p99": round(pct(http, 99) * 1e3, 3),
                                    "n": len(http), "note": "POST work_generate -> reply at the JSON boundary "

@@ -99,3 +99,47 @@ def test_bench_rank_sees_only_its_gpu(preset, local_rank, want):
     out = subprocess.run([sys.executable, "-c", "import os, bench; print(os.environ['HIP_VISIBLE_DEVICES'])"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=120, check=True)
     assert out.stdout.strip() == want
+
+
+def _node_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import bench
+    from fake_engine import OracleEngine
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # rank 1 is slow (sleeps between chunks), so rank 0 wins most roots and must cancel rank 1
+    eng = OracleEngine(chunk=1 << 10, delay=0.0 if rank == 0 else 0.002)
+    out = bench.node_time_to_work(eng, 0, rank, world, dist, 12, thr=0xfff0000000000000)
+    q.put((rank, out, [(c[2] % (1 << 64)) for c in eng.calls]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_node_time_to_work_cross_rank_first_win():
+    """bench.node_time_to_work: every root searched by both ranks on disjoint strides, the first win
+    cancelling the other rank's search through the shared-memory word."""
+    import glob
+    import tempfile
+    pattern = os.path.join(tempfile.gettempdir(), "nanopow_bench_cancel_*")
+    before = set(glob.glob(pattern))
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_node_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = {}
+    for _ in range(2):
+        r, out, starts = q.get(timeout=180)
+        got[r] = (out, starts)
+    for p in procs:
+        p.join(60)
+        assert p.exitcode == 0
+    out = got[0][0]
+    assert got[1][0] is None and out["n"] == 12 and out["failed"] == 0 and out["shared_cancel"]
+    assert out["p50"] > 0 and out["p99"] >= out["p50"]
+    assert out["rank_searches_cancelled"] >= 6  # the slow rank is cancelled by the winner's word
+    # disjoint strides: rank 1 starts half the nonce space away from rank 0, root by root
+    for s0, s1 in zip(got[0][1], got[1][1]):
+        assert (s1 - s0) % (1 << 64) == 1 << 63
+    assert set(glob.glob(pattern)) == before  # the shared file is unlinked at the end
