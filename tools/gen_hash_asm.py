@@ -261,7 +261,8 @@ def lower(dag: Dag, out: Node):
 
 # issue cost (SIMD cycles per wave64 instruction, profiles/r01_valu_ubench.json) and latency model
 COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b32": 4.3, "v_lshl_add_u64": 4.4,
-        "v_lshrrev_b32": 2.5, "v_mov_b32": 2.4, "v_add_co_u32": 2.1, "v_addc_co_u32": 2.1, "v_mad_u32_u24": 4.0}
+        "v_lshrrev_b32": 2.5, "v_mov_b32": 2.4, "v_add_co_u32": 2.1, "v_addc_co_u32": 2.1, "v_mad_u32_u24": 4.0,
+        "v_bitop3_b32": 2.5}
 # 64-bit add as v_add_co_u32 + v_addc_co_u32 (carry through VCC) instead of one v_lshl_add_u64:
 # both issue at full rate next to xors (profiles/r01_valu_mix2.jsonl), v_lshl_add_u64 does not
 ADD_CC = False
@@ -829,9 +830,54 @@ def allocate_and_emit(order: List[Ins], vrs: List[VR], base: int, limit: int, vo
 
 # ---------------------------------------------------------------------------------------
 # A tiny interpreter of the emitted text, to check the generator itself against hashlib.
+def fuse_output_xor(lines: List[str], counts: Dict[str, int]) -> List[str]:
+    """value = H0 ^ (v0 ^ v8): the stream ends, per half, in `v_xor_b32_e64 t, a, b` and
+    `v_xor_b32 %[value_*], <H0 literal>, t`.  Fold each pair into one 3-input
+    `v_bitop3_b32 %[value_*], a, b, %[h0_*] bitop3:0x96` (x ^ y ^ z) with the H0 half in an SGPR
+    (VOP3 takes no literal on gfx950): 2 instructions fewer per nonce.  Applied only where t is
+    read by nothing else and a, b are not rewritten between t's definition and the output."""
+    out = list(lines)
+
+    def dst(ln):
+        return ln.split(" ", 1)[1].split(",")[0].strip()
+
+    def srcs(ln):
+        return [t.strip().split(" ")[0] for t in ln.split(" ", 1)[1].split(",")[1:]]
+
+    for half, name in ((0, "value_lo"), (1, "value_hi")):
+        k = next((i for i, ln in enumerate(out) if ln.startswith("v_xor_b32 ") and dst(ln) == f"%[{name}]"), None)
+        if k is None:
+            continue
+        lit, t = srcs(out[k])
+        if not (lit.startswith("0x") and int(lit, 16) == (H0 >> (32 * half)) & M32 and t.startswith("v")):
+            continue
+        d = max((i for i in range(k) if dst(out[i]) == t or dst(out[i]).startswith("v[")
+                 and t in _pair_regs(dst(out[i]))), default=None)
+        if d is None or not out[d].startswith("v_xor_b32_e64 "):
+            continue
+        a, b = srcs(out[d])
+        between = out[d + 1:k]
+        if any(t in srcs(ln) for ln in between + out[k + 1:]):
+            continue
+        if any(dst(ln) in (a, b) or (dst(ln).startswith("v[") and {a, b} & set(_pair_regs(dst(ln))))
+               for ln in between):
+            continue
+        out[k] = f"v_bitop3_b32 %[{name}], {a}, {b}, %[h0_{'lo' if half == 0 else 'hi'}] bitop3:0x96"
+        del out[d]
+        counts["v_xor_b32"] -= 2
+        counts["v_bitop3_b32"] = counts.get("v_bitop3_b32", 0) + 1
+    return out
+
+
+def _pair_regs(tok: str) -> List[str]:
+    lo, hi = tok[2:-1].split(":")
+    return [f"v{r}" for r in range(int(lo), int(hi) + 1)]
+
+
 def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
     regs: Dict[int, int] = {}
-    named: Dict[str, int] = {"nonce_lo": nonce & M32, "nonce_hi": nonce >> 32, "k8": 1 << 8, "k16": 1 << 16}
+    named: Dict[str, int] = {"nonce_lo": nonce & M32, "nonce_hi": nonce >> 32, "k8": 1 << 8, "k16": 1 << 16,
+                             "h0_lo": H0 & M32, "h0_hi": H0 >> 32}
     for i, u in enumerate(uni_vals):
         named[f"u{i}_lo"] = u & M32
         named[f"u{i}_hi"] = u >> 32
@@ -874,6 +920,10 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
         ops = [t.strip() for t in rest.split(",")]
         if opc == "v_xor_b32":
             wr32(ops[0], rd32(ops[1]) ^ rd32(ops[2]))
+        elif opc == "v_bitop3_b32":
+            last, mod = ops[3].split(" ", 1)
+            assert mod.strip() == "bitop3:0x96", ln  # x ^ y ^ z
+            wr32(ops[0], rd32(ops[1]) ^ rd32(ops[2]) ^ rd32(last))
         elif opc == "v_alignbit_b32":
             hi, lo, sh = rd32(ops[1]), rd32(ops[2]), int(ops[3])
             wr32(ops[0], (((hi << 32) | lo) >> sh) & M32)
@@ -962,9 +1012,10 @@ def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List
         clobbers += ', "vcc"'
     ops_in = []
     for nm, expr in [("nonce", "nonce"), ("nonce_lo", "(uint32_t)nonce"), ("nonce_hi", "(uint32_t)(nonce >> 32)"),
-                     ("k8", "256u"), ("k16", "65536u")]:
+                     ("k8", "256u"), ("k16", "65536u"),
+                     ("h0_lo", f"0x{H0 & M32:08x}u"), ("h0_hi", f"0x{H0 >> 32:08x}u")]:
         if f"%[{nm}]" in text:
-            ops_in.append(f'[{nm}] "{"s" if nm.startswith("k") else "v"}"({expr})')
+            ops_in.append(f'[{nm}] "{"s" if nm.startswith(("k", "h0")) else "v"}"({expr})')
     for i in range(nu):
         if f"%[u{i}]" in text:
             ops_in.append(f'[u{i}] "s"(u[{i}])')
@@ -1031,6 +1082,8 @@ def main() -> int:
     ap.add_argument("--enc", choices=["vop3", "vop2"], default="vop3",
                     help="encoding of the simple 32-bit ops (xor, lshrrev)")
     ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
+    ap.add_argument("--fuse-out", choices=["bitop3", "none"], default="bitop3",
+                    help="fold the output xors H0 ^ (v0 ^ v8) into v_bitop3_b32 (fuse_output_xor)")
     ap.add_argument("--pad", choices=["odd", "even", "none"], default="odd",
                     help="placement of the stream: 4 (mod 8) [odd], 0 (mod 8) [even], or as it falls")
     args = ap.parse_args()
@@ -1056,6 +1109,8 @@ def main() -> int:
     else:
         order = schedule(ops, args.sched)
         lines, _uni, vmax, counts = emit(order, frontier, out, args.base, args.limit)
+    if args.fuse_out == "bitop3":
+        lines = fuse_output_xor(lines, counts)
     est = 0.0
     for ln in lines:
         opc = ln.split(" ", 1)[0]
@@ -1080,7 +1135,8 @@ def main() -> int:
     host_prog = c_expr_program(frontier)
     write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --add {args.add} --enc {args.enc}"
               + (f" --rotmad {args.rotmad}" if args.rotmad != "none" else "") + (" --swapmov" if args.swapmov else "")
-              + (f" --lat {args.lat:g} --window {args.window}" if args.sched == "ilp" else "") + f" --pad {args.pad}", est)
+              + (f" --lat {args.lat:g} --window {args.window}" if args.sched == "ilp" else "") + f" --pad {args.pad}"
+              + (" --fuse-out none" if args.fuse_out == "none" else ""), est)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
           f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")
     return 0

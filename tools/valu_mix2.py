@@ -165,6 +165,7 @@ def real_stream(path=None):
     out = []
     for ln in re.findall(r'"(.*?)\\n"', asm):
         ln = ln.replace("%[k8]", "s38").replace("%[k16]", "s39")
+        ln = ln.replace("%[h0_lo]", "s36").replace("%[h0_hi]", "s37")
         ln = ln.replace("%[nonce_lo]", "v56").replace("%[nonce_hi]", "v57")
         ln = ln.replace("%[nonce]", "v[56:57]").replace("%[value_lo]", "v58").replace("%[value_hi]", "v59")
         ln = re.sub(r"%\[u(\d+)_lo\]", lambda m: f"s{40 + 2 * int(m.group(1)) % 30}", ln)
@@ -179,7 +180,7 @@ def main():
     budget_us = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
     n_body = 360
     clob = ", ".join(f'"v{r}"' for r in range(8, 64))
-    sclob = ", ".join(f'"s{r}"' for r in range(38, 70))
+    sclob = ", ".join(f'"s{r}"' for r in range(36, 70))
     kernels, runs = [], []
     items = list(PATTERNS.items()) + [("real hash stream", None)]
     # extra generated streams: MIX_STREAMS="name=path.inc,name2=path2.inc"
