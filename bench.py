@@ -74,10 +74,10 @@ SEND = 0xfffffff800000000
 OPS_PER_NONCE = 2232                # int32 VALU ops of one 12-round compression
 PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # MI355X: 256 CU x (4 SIMD x 32 lanes) x 2.4 GHz = 78.6 Tops/s
 # The instruction stream's own issue bound (informational, next to the roofline): the generated hash
-# costs 5,727 SIMD cycles per wave (64 nonces) with every SIMD saturated and no launch tail
-# (tools/valu_mix2.py "real hash stream"/"stream seq", profiles/r01_valu_mix2_timebudget.jsonl):
-# 1,673 instructions, half of them half rate, at 3.42 cycles each.
-STREAM_CYCLES_PER_HASH = 5727
+# costs 5,725 SIMD cycles per wave (64 nonces) with every SIMD saturated and no launch tail
+# (tools/valu_mix2.py "real hash stream", 20-ms budget, two runs: profiles/r01_valu_mix2_final_stream.jsonl):
+# 1,671 instructions, half of them half rate, at 3.426 cycles each.
+STREAM_CYCLES_PER_HASH = 5725
 STREAM_CLOCK_GHZ = 2.39   # in-kernel s_memtime / s_memrealtime under this load
 STREAM_BOUND_GNPS = 1024 * 64 * STREAM_CLOCK_GHZ / STREAM_CYCLES_PER_HASH  # 1,024 SIMDs: 27.35
 METRIC = "Gnonce/s blake2b-64 per GPU & 8-GPU node; p50 time-to-work at fffffff8"
@@ -385,7 +385,7 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
                 "gnps": round(STREAM_BOUND_GNPS, 3),
                 "kernel_frac": (round(kern_nonces / (kern_ms * 1e-3) / 1e9 / STREAM_BOUND_GNPS, 4)
                                 if kern_ms > 0 else None),
-                "what": "measured issue bound of the generated 1,673-instruction stream (5,727 SIMD "
+                "what": "measured issue bound of the generated 1,671-instruction stream (5,725 SIMD "
                         "cycles per 64 nonces at 2.39 GHz, no launch tail; tools/valu_mix2.py): the "
                         "roofline frac is capped near 0.78 by its half-rate share, not by the kernel",
             },
