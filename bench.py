@@ -134,16 +134,40 @@ class NodeQueue:
     stream, every GPU stays busy until the N*K searches are done; ranks finish within about one
     search of each other."""
 
-    def __init__(self, dist, rank: int, total: int):
+    @staticmethod
+    def create(dist, rank: int, total: int):
+        """The queue, or None on every rank if any rank cannot use the file (the ranks then fall
+        back to K fixed roots each): every rank runs the same collectives either way."""
         import tempfile
+        import torch
         box = [None]
         if rank == 0:
-            fd, path = tempfile.mkstemp(prefix="nanopow_bench_queue_")
-            os.write(fd, (0).to_bytes(8, "little"))
-            os.close(fd)
-            box = [path]
+            try:
+                fd, path = tempfile.mkstemp(prefix="nanopow_bench_queue_")
+                os.write(fd, (0).to_bytes(8, "little"))
+                os.close(fd)
+                box = [path]
+            except OSError:
+                box = [None]
         dist.broadcast_object_list(box, src=0)
-        self.path, self.total, self.rank = box[0], total, rank
+        q = None
+        if box[0] is not None:
+            try:
+                q = NodeQueue(box[0], rank, total)
+            except OSError:
+                q = None
+        ok = torch.tensor([1 if q is not None else 0], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok[0]) == 1:
+            return q
+        if q is not None:
+            q.close()
+        elif rank == 0 and box[0] is not None:
+            os.unlink(box[0])
+        return None
+
+    def __init__(self, path: str, rank: int, total: int):
+        self.path, self.total, self.rank = path, total, rank
         self.fd = os.open(self.path, os.O_RDWR)
 
     def draw(self):
@@ -158,9 +182,12 @@ class NodeQueue:
         return i if i < self.total else None
 
     def close(self):
-        os.close(self.fd)
-        if self.rank == 0:
-            os.unlink(self.path)
+        try:
+            os.close(self.fd)
+            if self.rank == 0:
+                os.unlink(self.path)
+        except OSError:
+            pass
 
 
 class SharedWords:
@@ -289,7 +316,7 @@ def run_timed(search, stats, reset_stats, steps: int, warmup: int, rank: int, wo
         search(base_idx + 900_000 + w)
     reset_stats()
     one_node = int(os.environ.get("LOCAL_WORLD_SIZE", str(world))) == world
-    queue = NodeQueue(dist, rank, world * steps) if (dist is not None and world > 1 and one_node) else None
+    queue = NodeQueue.create(dist, rank, world * steps) if (dist is not None and world > 1 and one_node) else None
     if dist is not None:
         dist.barrier()
     # npow_search returns only after its streams drained, so the GPU is idle at both barriers
