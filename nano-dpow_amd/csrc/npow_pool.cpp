@@ -43,6 +43,11 @@ namespace {
 
 constexpr int kPending = 100;  // job status before it is decided
 constexpr double kYieldMinUs = 1500.0;  // yield a running launch only if more budget than this is left
+// ... and only if it holds fewer live unbounded jobs than this.  A new job then waits at most one
+// launch budget (20 ms), small beside its time-to-work when it shares the GPU with 8+ others
+// (>= 8 x ~19 ms at fffffff8), and a burst (64 live jobs, a win every ~20 ms) no longer ends
+// every launch early: each early end costs the GPU the gap before the next launch starts.
+constexpr int kYieldMaxLive = 8;
 constexpr int kIdleSpinUs = 2000;       // an idle worker polls for new jobs this long before sleeping
 constexpr double kPrelaunchUs = 2000.0;  // queue the next launch when the running one has this much budget left
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
@@ -265,6 +270,10 @@ void Worker::yield_if_long() {
                                                   std::chrono::steady_clock::now() - front_start_).count();
   NPOW_DBG("nanopow[%d]: yield? inflight %zu left_us %.0f\n", d_.id, q_.size(), left_us);
   if (q_.size() < 2 && left_us < kYieldMinUs) return;
+  int live = 0;
+  for (const Slot& sl : slots_)
+    if (sl.state == SlotState::kActive && !sl.fresh && !sl.job->max_per_dev) ++live;
+  if (live >= kYieldMaxLive) return;
   bool any = false;
   for (Slot& sl : slots_) {
     if (sl.state != SlotState::kActive || sl.fresh || sl.job->max_per_dev) continue;
