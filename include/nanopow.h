@@ -21,6 +21,9 @@
  *     `if (blake2b(attempt_l, item_a) >= difficulty)`).
  *   - Buffers are caller-owned; the library keeps no pointer past a call
  *     (the `cancel` word is read only while the call runs).
+ *   - A cancel word is raised from another thread with a release store
+ *     (`__atomic_store_n(w, 1, __ATOMIC_RELEASE)`; an aligned 32-bit store, as
+ *     ctypes makes, is one on x86-64); the library load-acquires it.
  *   - device_mask bit d selects HIP device d; 0 means "all devices".
  *   - Calls that use disjoint device sets may run concurrently from
  *     different threads; calls that share a device serialise on it.

@@ -1,6 +1,6 @@
-// Host AddressSanitizer driver for the C ABI (include/nanopow.h) -- TEST TOOL.
+// Host AddressSanitizer / ThreadSanitizer driver for the C ABI (include/nanopow.h) -- TEST TOOL.
 //
-// Built by `make -C nano-dpow_amd/csrc asan`: the engine, pool and kernel sources are
+// Built by `make -C nano-dpow_amd/csrc asan` (and `tsan`, tools/tsan.supp): the engine, pool and kernel sources are
 // compiled with -fsanitize=address on the host side only (device code untouched) and
 // linked straight into this executable, so the ASan runtime is part of the program
 // (a ctypes-loaded library cannot arrange that).  It drives every entry point the
@@ -68,7 +68,8 @@ static void tickets(int tid, int n) {
     uint64_t nonce = 0, value = 0, done = 0;
     rc = npow_wait(ticket, 2000, &nonce, &value, &done);
     if (rc == NPOW_PENDING) {
-      if (i & 1) cancel = 1; else npow_cancel(ticket);
+      if (i & 1) __atomic_store_n(&cancel, 1u, __ATOMIC_RELEASE);  // the library load-acquires it
+      else npow_cancel(ticket);
       rc = npow_wait(ticket, -1, &nonce, &value, &done);
     }
     CHECK(rc == NPOW_OK || rc == NPOW_CANCELLED, "ticket rc %d", rc);
