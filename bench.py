@@ -49,11 +49,14 @@ Other BASELINE.json configurations (``--workload``; not the driver's default lin
 from __future__ import annotations
 
 import argparse
+import ctypes
+import glob
 import hashlib
 import json
 import os
 import statistics
 import sys
+import threading
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -349,6 +352,66 @@ def run_timed(search, stats, reset_stats, steps: int, warmup: int, rank: int, wo
     dist.all_gather_object(gathered, ttw)
     all_ttw = [x for g in gathered for x in g]
     return int(v[0]), float(w_t[0]), all_ttw, float(v[1]), int(v[2]), int(v[3])
+
+
+class SclkSampler:
+    """Samples the shader clock of HIP device `dev` while the timed searches run (SURVEY.md §8(d):
+    report the roofline against the clock measured during the run, too).  The current DPM level
+    (the '*' line of the GPU's sysfs pp_dpm_sclk) is read every `period` seconds by a host thread;
+    the card is found by the PCI bus id the HIP runtime reports.  Reading sysfs touches no GPU
+    queue.  summary() is None when the file is unavailable."""
+
+    def __init__(self, dev: int, period: float = 0.05):
+        self.samples, self.bus, self.path = [], None, None
+        self.period, self._stop = period, threading.Event()
+        try:
+            hip = ctypes.CDLL("libamdhip64.so.7")
+            buf = ctypes.create_string_buffer(64)
+            if hip.hipDeviceGetPCIBusId(buf, ctypes.c_int(64), ctypes.c_int(dev)) == 0:
+                self.bus = buf.value.decode().lower()
+                for d in glob.glob("/sys/class/drm/card*/device"):
+                    if os.path.basename(os.path.realpath(d)).lower() == self.bus and \
+                            os.path.exists(os.path.join(d, "pp_dpm_sclk")):
+                        self.path = os.path.join(d, "pp_dpm_sclk")
+                        break
+        except (OSError, AttributeError):
+            self.path = None
+        self._thread = threading.Thread(target=self._run, daemon=True)
+
+    def _read(self):
+        with open(self.path) as f:
+            for ln in f:
+                if ln.rstrip().endswith("*"):
+                    return int(ln.split(":")[1].strip().split("M")[0])
+        return None
+
+    def _run(self):
+        while not self._stop.is_set():
+            try:
+                v = self._read()
+            except (OSError, ValueError, IndexError):
+                return
+            if v is not None:
+                self.samples.append(v)
+            self._stop.wait(self.period)
+
+    def __enter__(self):
+        if self.path:
+            self._thread.start()
+        return self
+
+    def __exit__(self, *exc):
+        self._stop.set()
+        if self._thread.is_alive():
+            self._thread.join()
+
+    def summary(self):
+        if not self.samples:
+            return None
+        return {"mean": round(statistics.mean(self.samples), 1), "min": min(self.samples),
+                "max": max(self.samples), "samples": len(self.samples),
+                "source": f"current level of pp_dpm_sclk of rank 0's GPU ({self.bus}), every "
+                          f"{int(self.period * 1e3)} ms over the warmup and timed searches"}
 
 
 def _pmc_traffic(name="r01_pmc_pool.json"):
@@ -930,13 +993,19 @@ def main() -> int:
         st = eng.stats(dev)
         return st.kernel_ms, st.nonces, st.launches
 
-    res = run_timed(search, stats, lambda: eng.reset_stats(dev), args.steps, args.warmup, rank, WORLD, dist)
+    with SclkSampler(dev) as sclk:
+        res = run_timed(search, stats, lambda: eng.reset_stats(dev), args.steps, args.warmup, rank, WORLD, dist)
     http = _http_ttw(eng, args.http_requests) if (rank == 0 and WORLD == 1 and args.http_requests) else None
     node = None
     if dist is not None and args.node_searches > 0 and int(os.environ.get("LOCAL_WORLD_SIZE", WORLD)) == WORLD:
         node = node_time_to_work(eng, dev, rank, WORLD, dist, args.node_searches)
     if rank == 0:
         line = result_line(WORLD, args.steps, args.warmup, *res)
+        clk = sclk.summary()
+        line["sclk_mhz"] = clk
+        if clk:
+            peak_at_clk = 256 * 128 * clk["mean"] * 1e6 / 1e12
+            line["roofline"]["frac_at_measured_sclk"] = round(line["roofline"]["achieved"] / peak_at_clk, 4)
         if node:
             line["node_ttw_ms"] = node
         if http:
