@@ -42,6 +42,7 @@ import argparse
 import hashlib
 import os
 import random
+import re
 import sys
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
@@ -266,6 +267,20 @@ COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b3
 # 64-bit add as v_add_co_u32 + v_addc_co_u32 (carry through VCC) instead of one v_lshl_add_u64:
 # both issue at full rate next to xors (profiles/r01_valu_mix2.jsonl), v_lshl_add_u64 does not
 ADD_CC = False
+# --add sgpr: the same carry pair in VOP3 form with its carry in an SGPR pair taken round-robin from
+# CARRY_SGPRS (v_add_co_u32_e64 v, s[k:k+1], ... / v_addc_co_u32_e64 v, s[k:k+1], ..., s[k:k+1]),
+# so consecutive adds do not all write and read VCC
+ADD_SGPR = False
+CARRY_SGPRS: List[int] = [20, 22, 24, 26]
+_carry_turn = [0]
+
+
+def next_carry() -> str:
+    k = CARRY_SGPRS[_carry_turn[0] % len(CARRY_SGPRS)]
+    _carry_turn[0] += 1
+    return f"s[{k}:{k + 1}]"
+
+
 ROT_MAD = lambda n, h: False  # which rotr16/24 halves use v_lshrrev_b32 + v_mad_u32_u24 (--rotmad)
 ROTL1_CC = False  # rotr63 = x + x + carry as v_add_co_u32 + 2x v_addc_co_u32
 ROTL1_VIA_ADD = True  # rotr63 = (x << 1) + (x >> 63): v_lshrrev_b32 + v_lshl_add_u64 with a zero partner
@@ -454,13 +469,19 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
                 x, y = y, x
             # v_addc reads VCC over the constant bus, which gfx950 allows only one read per
             # instruction: an add with an SGPR/literal operand stays one v_lshl_add_u64
-            cc = ADD_CC and not (a.uniform or b.uniform)
+            cc = (ADD_CC or ADD_SGPR) and not (a.uniform or b.uniform)
             hx = [half(x, 0), half(x, 1)] if cc else None
             hy = [half(y, 0), half(y, 1)] if cc else None
             consume(op)
             r = al.take2()
             loc[op.dst.id] = r
-            if cc:
+            if cc and ADD_SGPR:
+                c = next_carry()
+                lines.append(f"v_add_co_u32_e64 v{r}, {c}, {hx[0]}, {hy[0]}")
+                lines.append(f"v_addc_co_u32_e64 v{r + 1}, {c}, {hx[1]}, {hy[1]}, {c}")
+                cnt("v_add_co_u32")
+                cnt("v_addc_co_u32")
+            elif cc:
                 lines.append(f"v_add_co_u32 v{r}, vcc, {hx[0]}, {hy[0]}")
                 lines.append(f"v_addc_co_u32 v{r + 1}, vcc, {hx[1]}, {hy[1]}, vcc")
                 cnt("v_add_co_u32")
@@ -508,9 +529,15 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             r = al.take2()
             lines.append(f"v_xor_b32 v{r}, {s0l}, {s1l}")
             lines.append(f"v_xor_b32 v{r + 1}, {s0h}, {s1h}")
-            lines.append(f"v_add_co_u32 v{r}, vcc, v{r}, v{r}")
-            lines.append(f"v_addc_co_u32 v{r + 1}, vcc, v{r + 1}, v{r + 1}, vcc")
-            lines.append(f"v_addc_co_u32 v{r}, vcc, 0, v{r}, vcc")
+            if ADD_SGPR:
+                c = next_carry()
+                lines.append(f"v_add_co_u32_e64 v{r}, {c}, v{r}, v{r}")
+                lines.append(f"v_addc_co_u32_e64 v{r + 1}, {c}, v{r + 1}, v{r + 1}, {c}")
+                lines.append(f"v_addc_co_u32_e64 v{r}, {c}, 0, v{r}, {c}")
+            else:
+                lines.append(f"v_add_co_u32 v{r}, vcc, v{r}, v{r}")
+                lines.append(f"v_addc_co_u32 v{r + 1}, vcc, v{r + 1}, v{r + 1}, vcc")
+                lines.append(f"v_addc_co_u32 v{r}, vcc, 0, v{r}, vcc")
             loc[op.dst.id] = r
             cnt("v_xor_b32")
             cnt("v_xor_b32")
@@ -911,7 +938,7 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
         else:
             regs[int(tok[1:])] = val & M32
 
-    vcc = 0
+    carry: Dict[str, int] = {}  # "vcc" or "s[k:k+1]" -> the carry bit it holds
     for ln in lines:
         if ln.startswith(".") or ln.startswith("s_nop"):
             continue  # placement directives / padding
@@ -934,15 +961,15 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
         elif opc == "v_mad_u32_u24":
             wr32(ops[0], (rd32(ops[1]) & 0xffffff) * (rd32(ops[2]) & 0xffffff) + rd32(ops[3]))
         elif opc == "v_add_co_u32":
-            assert ops[1] == "vcc"
+            assert ops[1] == "vcc" or ops[1].startswith("s[")
             t = rd32(ops[2]) + rd32(ops[3])
             wr32(ops[0], t)
-            vcc = t >> 32
+            carry[ops[1]] = t >> 32
         elif opc == "v_addc_co_u32":
-            assert ops[1] == "vcc" and ops[4] == "vcc"
-            t = rd32(ops[2]) + rd32(ops[3]) + vcc
+            assert ops[1] == "vcc" or ops[1].startswith("s[")
+            t = rd32(ops[2]) + rd32(ops[3]) + carry[ops[4]]
             wr32(ops[0], t)
-            vcc = t >> 32
+            carry[ops[1]] = t >> 32
         elif opc == "v_lshl_add_u64":
             x = (rd64(ops[1]) << int(ops[2])) & M64
             y = rd64(ops[3])
@@ -1010,6 +1037,8 @@ def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List
     text = "\n".join(lines)
     if "vcc" in text:
         clobbers += ', "vcc"'
+    for k in sorted({int(m) for m in re.findall(r"s\[(\d+):\d+\]", text)}):
+        clobbers += f', "s{k}", "s{k + 1}"'
     ops_in = []
     for nm, expr in [("nonce", "nonce"), ("nonce_lo", "(uint32_t)nonce"), ("nonce_hi", "(uint32_t)(nonce >> 32)"),
                      ("k8", "256u"), ("k16", "65536u"),
@@ -1075,8 +1104,11 @@ def main() -> int:
     ap.add_argument("--rotl1", choices=["add", "alignbit", "cc"], default="add",
                     help="rotr63 as v_lshrrev_b32 + v_lshl_add_u64 (add), two v_alignbit_b32, or a "
                          "v_add_co_u32 + 2x v_addc_co_u32 carry chain (cc)")
-    ap.add_argument("--add", choices=["u64", "cc"], default="u64",
-                    help="64-bit add as one v_lshl_add_u64 (u64) or v_add_co_u32 + v_addc_co_u32 (cc)")
+    ap.add_argument("--add", choices=["u64", "cc", "sgpr"], default="u64",
+                    help="64-bit add as one v_lshl_add_u64 (u64) or v_add_co_u32 + v_addc_co_u32 with the "
+                         "carry in VCC (cc) or in SGPR pairs taken round-robin (sgpr, --carry-sgprs)")
+    ap.add_argument("--carry-sgprs", default="20,22,24,26",
+                    help="sgpr: even SGPRs whose pairs carry the adds (round-robin)")
     ap.add_argument("--rotmad", choices=["none", "lo", "hi", "both", "r16", "r24", "r16lo", "r24lo"], default="none",
                     help="rotr16/rotr24 halves as v_lshrrev_b32 + v_mad_u32_u24 instead of v_alignbit_b32")
     ap.add_argument("--enc", choices=["vop3", "vop2"], default="vop3",
@@ -1089,6 +1121,9 @@ def main() -> int:
     args = ap.parse_args()
     global ROTL1_VIA_ADD, VOP3_SIMPLE, SWAP_MOV, PAD, ADD_CC, ROTL1_CC
     ADD_CC = args.add == "cc"
+    global ADD_SGPR, CARRY_SGPRS
+    ADD_SGPR = args.add == "sgpr"
+    CARRY_SGPRS = [int(x) for x in args.carry_sgprs.split(",")]
     global ROT_MAD
     ROT_MAD = {"none": lambda n, h: False, "lo": lambda n, h: h == 0, "hi": lambda n, h: h == 1,
                "both": lambda n, h: True, "r16": lambda n, h: n == 16, "r24": lambda n, h: n == 24,

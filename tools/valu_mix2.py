@@ -32,6 +32,9 @@ PATTERNS = {
     "xor dep x4 chains": ["xordep4"],
     "alignbyte": ["alignbyte"], "alignbyte2": ["alignbyte2"], "addco": ["addco"], "addc": ["addc"],
     "addco|addc": ["addco", "addc"], "addco3|addc3": ["addco3", "addc3"], "lshlor": ["lshlor"],
+    "addco4|addc4 sgpr-rot": ["addco4a", "addc4a"], "addco6 sgpr-rot": ["addco8"],
+    "xor xor|addco4 addc4 sgpr-rot": ["xor", "xor", "addco4b", "addc4b"],
+    "xor|addco6 sgpr-rot alt": ["xor", "addco8"],
     "lshl": ["lshl"], "or": ["or"], "lshr64": ["lshr64"], "add3": ["add3"], "addu": ["addu"],
     "xor|alignbyte alt": ["xor", "alignbyte"], "xor|lshlor alt": ["xor", "lshlor"],
     "xor xor|addco addc": ["xor", "xor", "addco", "addc"],
@@ -116,6 +119,15 @@ def emit2(kind, i):
         return f"v_add_co_u32_e64 v{d}, s[20:21], v{s0}, v{s1}"
     if kind == "addc3":
         return f"v_addc_co_u32_e64 v{d + 1}, s[20:21], v{s0 + 1}, v{s1 + 1}, s[20:21]"
+    if kind in ("addco4a", "addc4a", "addco4b", "addc4b"):
+        # carry in an SGPR pair rotating over s[20:21]..s[26:27]: a = pattern of 2 (co, c), b = of 4
+        k = 20 + 2 * ((i // (2 if kind.endswith("a") else 4)) % 4)
+        if kind.startswith("addco"):
+            return f"v_add_co_u32_e64 v{d}, s[{k}:{k + 1}], v{s0}, v{s1}"
+        return f"v_addc_co_u32_e64 v{d + 1}, s[{k}:{k + 1}], v{s0 + 1}, v{s1 + 1}, s[{k}:{k + 1}]"
+    if kind == "addco8":  # six rotating pairs, carry-out only
+        k = 20 + 2 * (i % 6)
+        return f"v_add_co_u32_e64 v{d}, s[{k}:{k + 1}], v{s0}, v{s1}"
     if kind == "lshlor":
         return f"v_lshl_or_b32 v{d}, v{s0}, 8, v{s1}"
     if kind == "lshl":
@@ -181,6 +193,7 @@ def main():
     n_body = 360
     clob = ", ".join(f'"v{r}"' for r in range(8, 64))
     sclob = ", ".join(f'"s{r}"' for r in range(36, 70))
+    cclob = ", ".join(f'"s{r}"' for r in range(20, 32))  # carry pairs of the SGPR-carry patterns / streams
     kernels, runs = [], []
     items = list(PATTERNS.items()) + [("real hash stream", None)]
     # extra generated streams: MIX_STREAMS="name=path.inc,name2=path2.inc"
@@ -206,7 +219,7 @@ __global__ __launch_bounds__(256) void mix_{k}(unsigned long long* out) {{
   const unsigned long long m0 = __builtin_amdgcn_s_memtime();
   asm volatile("v_mov_b32 v40, v0\\n\\tv_mov_b32 v52, v0\\n\\tv_mov_b32 v56, v0\\n\\tv_mov_b32 v57, 0" ::: {clob});
   do {{
-    asm volatile("{asm}" ::: {clob}, {sclob}, "vcc", "s20", "s21", "s22", "s23", "s24", "s25", "s26", "s27");
+    asm volatile("{asm}" ::: {clob}, {sclob}, "vcc", {cclob});
     ++n;
     asm volatile("s_memrealtime %0\\n\\ts_waitcnt lgkmcnt(0)" : "=s"(now) :: "memory");
   }} while (now - t0 < {budget_us * 100}ull);
