@@ -45,7 +45,7 @@ extern "C" {
 #define NPOW_ERR_NO_DEVICE (-2)
 #define NPOW_ERR_BAD_ARGUMENT (-3)
 #define NPOW_ERR_HIP (-4)
-#define NPOW_ERR_INVALID_WORK (-5) /* GPU result failed CPU re-validation 3 times in a row */
+#define NPOW_ERR_INVALID_WORK (-5) /* a job's last device was dropped for 3 invalid results in a row */
 #define NPOW_ERR_CAPACITY (-6)     /* sweep found more hits than `cap` (n_out still exact) */
 #define NPOW_ERR_INTERNAL (-7)     /* host-side failure (out of memory, thread creation); no C++
                                       exception ever crosses this ABI */
@@ -59,6 +59,15 @@ typedef struct npow_device_stats {
   uint64_t invalid_work;  /* GPU winners rejected by CPU re-validation */
   int32_t cus;            /* compute units */
   int32_t grid;           /* workgroups per search/sweep launch */
+  double clock_mhz;       /* in-kernel shader clock of the search launches since the last reset:
+                             s_memtime / s_memrealtime spans of one wave per XCD (0 = none yet) */
+  double host_cpu_ms;     /* CPU time of the device's pool worker thread since the last reset */
+  double host_wall_ms;    /* wall time since the last reset (host_cpu_ms / host_wall_ms = the
+                             worker's share of one core) */
+  int32_t dead;           /* 1 once the device has been dropped: 3 invalid results in a row
+                             (nano-work-server.exe @1669144) or a failed HIP call; searches then
+                             skip it and its jobs' remaining ranges move to the other devices */
+  int32_t reserved;
 } npow_device_stats;
 
 /* Open every visible HIP device, create its stream and buffers.

@@ -16,6 +16,9 @@
 // polls.  No collective: the only cross-GPU datum is the winner.
 #include <hip/hip_runtime.h>
 
+#include <pthread.h>
+#include <time.h>
+
 #include <algorithm>
 #include <exception>
 #include <chrono>
@@ -174,6 +177,45 @@ int check_init() {
   return NPOW_OK;
 }
 
+// Release one device's resources (any of them may be missing: a partial npow_init).
+void free_device(Device& d) {
+  (void)hipSetDevice(d.hip_id);
+  if (d.stream) (void)hipStreamSynchronize(d.stream);
+  for (int r = 0; r < kEventRing; ++r) {
+    if (d.ev_start[r]) (void)hipEventDestroy(d.ev_start[r]);
+    if (d.ev_stop[r]) (void)hipEventDestroy(d.ev_stop[r]);
+  }
+  if (d.st) (void)hipFree(d.st);
+  if (d.d_out) (void)hipFree(d.d_out);
+  if (d.mb) (void)hipHostFree(d.mb);
+  pool_device_free(d);
+  if (d.stream) (void)hipStreamDestroy(d.stream);
+}
+
+// Create one device's stream, buffers and events (d is already in g_devs).
+int init_device(Device& d, int n_physical) {
+  d.hip_id = d.id % n_physical;
+  HIPTRY(hipSetDevice(d.hip_id));
+  hipDeviceProp_t p;
+  HIPTRY(hipGetDeviceProperties(&p, d.hip_id));
+  d.cus = p.multiProcessorCount;
+  HIPTRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  HIPTRY(hipMalloc(&d.st, sizeof(DevState)));
+  HIPTRY(hipMalloc(&d.d_out, kValuesChunk * sizeof(uint64_t)));
+  void* mb = nullptr;
+  HIPTRY(hipHostMalloc(&mb, sizeof(HostMailbox), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
+  memset(mb, 0, sizeof(HostMailbox));
+  d.mb = (HostMailbox*)mb;
+  void* mbd = nullptr;
+  HIPTRY(hipHostGetDevicePointer(&mbd, mb, 0));
+  d.mb_dev = (HostMailbox*)mbd;
+  for (int r = 0; r < kEventRing; ++r) {
+    HIPTRY(hipEventCreate(&d.ev_start[r]));
+    HIPTRY(hipEventCreate(&d.ev_stop[r]));
+  }
+  return pool_device_init(d);
+}
+
 // ---------------------------------------------------------------------------------------
 // Sweep one contiguous sub-range on one device; hits (unsorted) appended to `hits`.
 int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t start, uint64_t count,
@@ -264,29 +306,15 @@ int npow_init(int* n_devices) try {
     if (k > 0) n_logical = k;
   }
   for (int i = 0; i < n_logical && i < 64; ++i) {
-    auto d = std::make_unique<Device>();
-    d->id = i;
-    d->hip_id = i % n;
-    HIPTRY(hipSetDevice(d->hip_id));
-    hipDeviceProp_t p;
-    HIPTRY(hipGetDeviceProperties(&p, d->hip_id));
-    d->cus = p.multiProcessorCount;
-    HIPTRY(hipStreamCreateWithFlags(&d->stream, hipStreamNonBlocking));
-    HIPTRY(hipMalloc(&d->st, sizeof(DevState)));
-    HIPTRY(hipMalloc(&d->d_out, kValuesChunk * sizeof(uint64_t)));
-    void* mb = nullptr;
-    HIPTRY(hipHostMalloc(&mb, sizeof(HostMailbox), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
-    memset(mb, 0, sizeof(HostMailbox));
-    d->mb = (HostMailbox*)mb;
-    void* mbd = nullptr;
-    HIPTRY(hipHostGetDevicePointer(&mbd, mb, 0));
-    d->mb_dev = (HostMailbox*)mbd;
-    for (int r = 0; r < kEventRing; ++r) {
-      HIPTRY(hipEventCreate(&d->ev_start[r]));
-      HIPTRY(hipEventCreate(&d->ev_stop[r]));
+    g_devs.push_back(std::make_unique<Device>());
+    g_devs.back()->id = i;
+    if (int rc = init_device(*g_devs.back(), n)) {
+      // leave nothing behind: a retried npow_init starts from an empty device list
+      const std::string msg = last_error();
+      for (auto& d : g_devs) free_device(*d);
+      g_devs.clear();
+      return fail(rc, msg);
     }
-    if (int rc = pool_device_init(*d)) return rc;
-    g_devs.push_back(std::move(d));
   }
   g_init = true;
   pool_start();
@@ -310,17 +338,7 @@ void npow_shutdown(void) try {
   if (g_init) pool_stop();
   for (auto& d : g_devs) {
     std::lock_guard<std::mutex> lk(d->mu);
-    (void)hipSetDevice(d->hip_id);
-    (void)hipStreamSynchronize(d->stream);
-    for (int r = 0; r < kEventRing; ++r) {
-      (void)hipEventDestroy(d->ev_start[r]);
-      (void)hipEventDestroy(d->ev_stop[r]);
-    }
-    (void)hipFree(d->st);
-    (void)hipFree(d->d_out);
-    (void)hipHostFree(d->mb);
-    pool_device_free(*d);
-    (void)hipStreamDestroy(d->stream);
+    free_device(*d);
   }
   g_devs.clear();
   g_init = false;
@@ -353,17 +371,32 @@ int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu) try {
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 
+// CPU time (ms) the device's pool worker thread has used so far (0 if unavailable).
+static double worker_cpu_ms(Device& d) {
+  if (!d.worker.joinable()) return 0.0;
+  clockid_t cid;
+  timespec ts;
+  if (pthread_getcpuclockid(d.worker.native_handle(), &cid) != 0 || clock_gettime(cid, &ts) != 0) return 0.0;
+  return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
 int npow_device_stats_get(int device, npow_device_stats* out) try {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size() || !out) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
   Device& d = *g_devs[device];
+  const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
+  *out = npow_device_stats{};
   out->launches = d.launches;
   out->nonces = d.nonces;
   out->kernel_ms = d.kernel_ms;
   out->invalid_work = d.invalid;
   out->cus = d.cus;
   out->grid = pool_grid_of(d);
+  out->clock_mhz = d.clk_ref_ticks > 0 ? d.clk_ticks / d.clk_ref_ticks * 100.0 : 0.0;
+  out->host_cpu_ms = cpu - d.worker_cpu0_ms;
+  out->host_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d.stats_t0).count();
+  out->dead = d.dead ? 1 : 0;
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 
@@ -371,9 +404,13 @@ int npow_device_stats_reset(int device) try {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size()) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
   Device& d = *g_devs[device];
+  const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
   d.launches = d.nonces = d.invalid = 0;
   d.kernel_ms = 0.0;
+  d.clk_ticks = d.clk_ref_ticks = 0.0;
+  d.stats_t0 = std::chrono::steady_clock::now();
+  d.worker_cpu0_ms = cpu;
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 

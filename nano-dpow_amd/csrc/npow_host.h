@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <atomic>
+#include <chrono>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -28,6 +29,7 @@ const std::string& last_error();
   } while (0)
 
 constexpr int kEventRing = 4;
+static_assert(kEventRing == sizeof(PoolMailbox::clk) / sizeof(PoolMailbox::clk[0]), "one clock record set per ring");
 
 struct Device {
   int id = 0;       // logical index (device_mask bit)
@@ -55,7 +57,14 @@ struct Device {
   std::mutex stats_mu;
   uint64_t launches = 0, nonces = 0, invalid = 0;
   double kernel_ms = 0.0;
+  double clk_ticks = 0.0, clk_ref_ticks = 0.0;  // in-kernel s_memtime / s_memrealtime spans (stats)
+  std::chrono::steady_clock::time_point stats_t0 = std::chrono::steady_clock::now();
+  double worker_cpu0_ms = 0.0;                   // the pool worker's thread CPU time at the last reset
+  // Dropped (dead) devices: select_devices() skips them; set once, by the device's worker (or
+  // npow_init) -- 3 invalid results in a row or a failed HIP call (npow_pool.cpp, fault policy).
   std::atomic<bool> dead{false};
+  int dead_code = NPOW_ERR_HIP;  // the error a job gets when no device is left to search it
+  std::string dead_msg;
 };
 
 extern std::vector<std::unique_ptr<Device>> g_devs;

@@ -110,7 +110,9 @@ struct PoolTable {
                        // together); 0 = iteration count only
   uint64_t yield_base;    // PoolMailbox::yield when the table was built: a polling wave that
                           // reads a different value ends the launch's unbounded entries
-  uint32_t pad[10];
+  uint32_t ring;          // PoolMailbox::clk[ring]: this launch's clock records ...
+  uint32_t seq;           // ... tagged with the launch's sequence number (low 32 bits)
+  uint32_t pad[8];
   PoolEntry e[kMaxSlots];
 };
 inline size_t pool_table_bytes(uint32_t n) { return offsetof(PoolTable, e) + (size_t)n * sizeof(PoolEntry); }
@@ -142,10 +144,19 @@ struct alignas(64) PoolWin {
   uint64_t value;
   uint8_t pad[40];
 };
+// In-kernel clock of a search launch: the first wave of workgroups 0..7 (one per XCD) records
+// its s_memtime span (shader cycles) and s_memrealtime span (100 MHz) from its first to its
+// last instruction; clock = cycles / ref * 100 MHz.  Written only here, read only by the host.
+constexpr int kClkWaves = 8;
+struct PoolClk {
+  uint64_t cycles, ref;
+  uint32_t seq, pad;
+};
 struct PoolMailbox {
   PoolWin win[kMaxSlots];
   uint64_t kill[kMaxSlots];  // kill[s] = gen: the job in slot s (that generation) must stop
   alignas(64) uint64_t yield;  // bumped by the host when new jobs wait for the next launch
+  alignas(64) PoolClk clk[4][kClkWaves];  // [launch ring][XCD] (host: kEventRing == 4)
 };
 
 // Launchers (defined in npow_kernel.hip).

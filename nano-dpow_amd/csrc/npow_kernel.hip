@@ -438,6 +438,23 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
 #endif
 }
 
+// Live in-kernel clock (PoolClk): the first wave of workgroups 0..kClkWaves-1 -- one per XCD,
+// workgroups are dealt to XCDs round-robin -- reads s_memtime after its first instruction and
+// both counters after its last; 2 scalar reads and one 24-byte store per 4,096 waves.
+__device__ __forceinline__ bool clk_wave() { return blockIdx.x < (unsigned)kClkWaves && threadIdx.x < 64; }
+__device__ __forceinline__ uint64_t clk_begin() { return clk_wave() ? __builtin_amdgcn_s_memtime() : 0; }
+__device__ __forceinline__ void clk_end(const PoolTable* tab, PoolMailbox* mb, uint64_t t_start, uint64_t c_start) {
+  if (!clk_wave()) return;
+  const uint64_t c_end = __builtin_amdgcn_s_memtime();
+  const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    PoolClk* r = &mb->clk[tab->ring & 3][blockIdx.x];
+    __hip_atomic_store(&r->cycles, c_end - c_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->ref, t_end - t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->seq, tab->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // The table in device memory (uploaded in stream order before the launch).
 template <bool BOUNDED>
 __global__ __launch_bounds__(kBlock)
@@ -448,7 +465,9 @@ void npow_pool_kernel(const PoolTable* __restrict__ tab, PoolDevState* __restric
                       PoolMailbox* __restrict__ mb) {
   uint64_t t_start;  // first instruction: see pool_body
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
+  const uint64_t c_start = clk_begin();
   pool_body<BOUNDED>(tab, st, mb, t_start);
+  clk_end(tab, mb, t_start, c_start);
 }
 
 // Up to kArgEntries entries: the table travels in the launch's kernel arguments, so no copy
@@ -465,7 +484,9 @@ void npow_pool_kernel_arg(const PoolTableArg targ, PoolDevState* __restrict__ st
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
   (void)targ;
   const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();  // address space 4 -> generic
+  const uint64_t c_start = clk_begin();
   pool_body<BOUNDED>(tab, st, mb, t_start);
+  clk_end(tab, mb, t_start, c_start);
 }
 
 hipError_t launch_pool(int grid, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,

@@ -7,8 +7,8 @@
 // (client/bin/windows/nano-work-server.exe, Rust source not vendored; behaviour from its
 // strings): requests queue FIFO (@1681064 `--shuffle` is the server's choice of order),
 // every GPU scans nonce chunks for the queued root, each GPU result is re-validated on the
-// CPU ("GPU returned invalid work", @1669040; a device is abandoned for the work after 3
-// in a row, @1669144), and work_cancel ends the request with "Cancelled" (@1673856).
+// CPU ("GPU returned invalid work", @1669040; a GPU is dropped after 3 invalid results in a
+// row, @1669144), and work_cancel ends the request with "Cancelled" (@1673856).
 // The reference serves ONE root at a time; a DPoW burst (many work_generate requests in
 // flight, client/work_handler.py:83-125 per client) is served here by keeping up to
 // kMaxSlots roots live in every launch, so a root that is won mid-launch costs nothing:
@@ -20,7 +20,18 @@
 // only cross-device datum is a job's outcome: the first device whose winner passes CPU
 // re-validation decides the job, the others raise their slot's kill word (pinned host
 // memory that the waves poll) and retire it.  No collective, no device-to-device traffic.
+//
+// Fault policy (per device, never per job): a device whose winners fail CPU re-validation 3
+// times in a row (across jobs), or whose HIP calls fail, is marked dead: select_devices()
+// skips it from then on, and every job it held hands the part of its nonce range the device
+// had not finished to the job's surviving devices (re-striding; a bounded job's range stays
+// covered exactly once more).  A job fails only when no device is left to search it.
+// Test hooks (environment, read once): NANOPOW_FAULT_INVALID=d[,d...] makes the host read a
+// corrupted value for every win of those logical devices; NANOPOW_FAULT_HIP=d:n makes device
+// d's launches fail after its n-th.
 #include <hip/hip_runtime.h>
+#include <sys/prctl.h>
+#include <time.h>
 
 #include <algorithm>
 #include <chrono>
@@ -30,6 +41,7 @@
 #include <cstring>
 #include <deque>
 #include <memory>
+#include <pthread.h>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -50,15 +62,57 @@ constexpr double kYieldMinUs = 1500.0;  // yield a running launch only if more b
 constexpr int kYieldMaxLive = 8;
 constexpr int kIdleSpinUs = 2000;       // an idle worker polls for new jobs this long before sleeping
 constexpr double kPrelaunchUs = 2000.0;  // queue the next launch when the running one has this much budget left
+constexpr double kFreshSpinUs = 400.0;   // poll without sleeping this long after a launch starts (quick wins)
+constexpr int kInvalidStreakMax = 3;     // consecutive invalid results that drop a device (@1669144)
+// Between steps a worker with a launch in flight sleeps this long (wakes early on new jobs):
+// a win is seen within it, and the thread costs a few % of a core instead of spinning.
+// NANOPOW_POLL_US overrides (0 = spin).
+const double g_poll_us = [] {
+  const char* e = getenv("NANOPOW_POLL_US");
+  return e ? atof(e) : 100.0;
+}();
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
 const bool g_trace_lat = getenv("NANOPOW_TRACE_LATENCY") != nullptr;
 double now_us() {
   return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
+// Fault injection (tests): see the header comment.
+struct Faults {
+  uint64_t invalid_mask = 0;  // logical devices whose wins read back corrupted
+  int hip_dev = -1;           // logical device whose launches fail ...
+  uint64_t hip_after = 0;     // ... after this many
+};
+const Faults& faults() {
+  static const Faults f = [] {
+    Faults x;
+    if (const char* e = getenv("NANOPOW_FAULT_INVALID")) {
+      for (const char* p = e; *p;) {
+        char* end = nullptr;
+        const long d = strtol(p, &end, 10);
+        if (end == p) break;
+        if (d >= 0 && d < 64) x.invalid_mask |= 1ull << d;
+        p = *end ? end + 1 : end;
+      }
+    }
+    if (const char* e = getenv("NANOPOW_FAULT_HIP")) {
+      char* end = nullptr;
+      x.hip_dev = (int)strtol(e, &end, 10);
+      if (end && *end == ':') x.hip_after = strtoull(end + 1, nullptr, 10);
+    }
+    return x;
+  }();
+  return f;
+}
+
 #define NPOW_DBG(...)                     \
   do {                                    \
     if (g_debug) fprintf(stderr, __VA_ARGS__); \
   } while (0)
+
+// [base, base + count) mod 2^64: nonces of a job still to be handed to launches
+struct Range {
+  uint64_t base, count;
+};
 
 struct Job {
   uint64_t ticket = 0;
@@ -66,16 +120,20 @@ struct Job {
   uint64_t u[NPOW_ASM_N_UNIFORMS] = {};
   uint64_t threshold = 0, start = 0, max_per_dev = 0, spacing = 0;
   const volatile uint32_t* cancel = nullptr;
-  std::vector<int> devs;  // device ids; the k-th scans from start + k * spacing
+  std::vector<int> devs;  // device ids; the k-th starts on [start + k * spacing, + stride)
   // guarded by g_pool.mu
-  std::vector<uint64_t> issued;     // per device k: nonces of its stride handed to launches
+  std::vector<std::deque<Range>> todo;  // per device k: ranges not yet handed to a launch (a dead
+                                        // device's remainder is re-strided onto the survivors')
   std::vector<uint8_t> on_dev;      // per device k: a slot holds the job
   std::vector<uint8_t> seen_dev;    // per device k: adopted at least once (re-adoptions do not yield)
   std::vector<uint8_t> dev_done;    // per device k: finished with the job
-  std::vector<int> invalid_streak;  // per device k
   int pending_devs = 0;
   bool admitted = false;
+  bool lost = false;                // a dead device's remainder had no surviving device to go to
+  int lost_code = NPOW_ERR_HIP;
   std::atomic<bool> finished{false};  // written under g_pool.mu; waiters may spin on it
+  std::condition_variable cv;         // its waiters (pool_wait), notified by finish_locked: one job's end
+                                      // wakes only its own waiters, not every thread blocked in npow_wait
   int status = kPending;
   uint64_t nonce = 0, value = 0, done = 0;
   std::string err;
@@ -92,7 +150,6 @@ using JobP = std::shared_ptr<Job>;
 struct Pool {
   std::mutex mu;
   std::condition_variable cv_work;  // workers: new admissions / shutdown
-  std::condition_variable cv_done;  // waiters: a job finished
   std::deque<JobP> waiting;
   std::vector<JobP> active;
   std::unordered_map<uint64_t, JobP> tickets;
@@ -133,7 +190,7 @@ void finish_locked(const JobP& j) {
   if (j->finished) return;
   if (j->status == kPending) {
     if (j->cancel_seen()) j->status = NPOW_CANCELLED;
-    else if (!j->err.empty()) j->status = NPOW_ERR_HIP;
+    else if (j->lost) j->status = j->lost_code;
     else j->status = NPOW_EXHAUSTED;
     j->decided = true;
   }
@@ -144,7 +201,7 @@ void finish_locked(const JobP& j) {
   auto wt = std::find(g_pool.waiting.begin(), g_pool.waiting.end(), j);
   if (wt != g_pool.waiting.end()) g_pool.waiting.erase(wt);
   admit_locked();
-  g_pool.cv_done.notify_all();
+  j->cv.notify_all();
 }
 
 // Device k of job j is finished with it (retired, exhausted, or the device failed).
@@ -153,6 +210,43 @@ void device_done_locked(const JobP& j, size_t k) {
   j->dev_done[k] = 1;
   j->on_dev[k] = 0;
   if (--j->pending_devs == 0) finish_locked(j);
+}
+
+// Device k of job j is dead: hand the ranges it had not finished (j->todo[k], including any a
+// failed launch pushed back) to the job's surviving devices, split evenly (re-striding), then
+// release it.  With no survivor the job has lost part of its nonce space and fails.
+void abandon_locked(const JobP& j, size_t k, int code, const std::string& msg) {
+  if (j->dev_done[k]) return;
+  std::deque<Range> rest;
+  rest.swap(j->todo[k]);
+  if (!j->decided && !rest.empty()) {
+    std::vector<size_t> surv;
+    for (size_t k2 = 0; k2 < j->devs.size(); ++k2)
+      if (k2 != k && !g_devs[(size_t)j->devs[k2]]->dead) surv.push_back(k2);
+    if (surv.empty()) {
+      j->lost = true;
+      j->lost_code = code;
+      j->err = msg;
+    } else {
+      const uint64_t S = surv.size();
+      for (const Range& r : rest) {
+        uint64_t off = 0;
+        for (uint64_t i = 0; i < S; ++i) {
+          const uint64_t part = r.count / S + (i < r.count % S ? 1 : 0);
+          if (part) j->todo[surv[i]].push_back({r.base + off, part});
+          off += part;
+        }
+      }
+      for (size_t k2 : surv)
+        if (j->dev_done[k2] && !j->todo[k2].empty()) {  // it had finished its own part: reopen
+          j->dev_done[k2] = 0;
+          ++j->pending_devs;
+        }
+      g_pool.version.fetch_add(1);
+      g_pool.cv_work.notify_all();
+    }
+  }
+  device_done_locked(j, k);
 }
 
 // -- one device's worker ------------------------------------------------------------------------
@@ -169,6 +263,10 @@ struct Slot {
   bool no_more = false;    // bounded range fully issued
   bool readback = false;   // done-shard read-back queued (ev_done[slot] marks it)
   bool fresh = false;      // adopted since the last launch was built
+  struct Issued {
+    uint64_t seq, base, count;
+  };
+  std::vector<Issued> inflight;  // ranges handed to launches that have not completed (in order)
 };
 
 struct PoolInflight {
@@ -190,6 +288,7 @@ class Worker {
   int ring_ = 0;
   std::chrono::steady_clock::time_point front_start_{};  // host estimate of the running launch's start
   uint64_t yields_ = 0;
+  int invalid_streak_ = 0;  // consecutive winners of this device that failed CPU re-validation
   std::unique_lock<std::mutex> dev_lock_{d_.mu, std::defer_lock};
 
   bool busy() const {
@@ -207,7 +306,10 @@ class Worker {
   int queue_readbacks();
   int retire();
   void fail_all(const std::string& msg);
+  void push_back_locked(Slot& sl, size_t from);
+  void account_clock(int ring, uint64_t seq);
   int step();
+  void nap();
 };
 
 int index_in(const Job& j, int dev) {
@@ -226,6 +328,7 @@ bool wants_device_locked(int dev) {
 }
 
 void Worker::adopt() {
+  if (d_.dead) return;  // draining before it releases its jobs (run())
   const uint64_t v = g_pool.version.load();
   if (v == seen_version_) return;
   bool adopted = false;
@@ -234,7 +337,7 @@ void Worker::adopt() {
   for (const JobP& j : std::vector<JobP>(g_pool.active)) {  // copy: device_done_locked may erase
     const int k = index_in(*j, d_.id);
     if (k < 0 || j->on_dev[k] || j->dev_done[k]) continue;
-    if (j->decided) {  // decided before this device got to it
+    if (j->decided || j->todo[k].empty()) {  // decided before this device got to it, or nothing left
       device_done_locked(j, k);
       continue;
     }
@@ -251,6 +354,7 @@ void Worker::adopt() {
     sl.gen = ++g_gen;
     sl.win_seen = sl.requeue = sl.no_more = sl.readback = false;
     sl.fresh = true;
+    sl.inflight.clear();
     j->on_dev[k] = 1;
     if (g_trace_lat && j->t_adopt == 0) j->t_adopt = now_us();
     if (!j->seen_dev[k]) adopted = true;  // a new job: worth ending a long launch for
@@ -295,27 +399,66 @@ void Worker::handle_win(int s) {
   PoolWin& pw = d_.pmb->win[s];
   sl.win_seen = true;
   const uint64_t n = __atomic_load_n(&pw.nonce, __ATOMIC_RELAXED);
-  const uint64_t v = __atomic_load_n(&pw.value, __ATOMIC_RELAXED);
+  uint64_t v = __atomic_load_n(&pw.value, __ATOMIC_RELAXED);
+  if ((faults().invalid_mask >> d_.id) & 1) v ^= 1;  // NANOPOW_FAULT_INVALID (tests)
   const uint64_t cpu_v = host_work_value(j.pre.m, n);
   std::lock_guard<std::mutex> g(g_pool.mu);
   if (g_trace_lat && j.t_win == 0) j.t_win = now_us();
   if (cpu_v == v && v >= j.threshold) {
-    j.invalid_streak[sl.k] = 0;
+    invalid_streak_ = 0;
     decide_locked(j, NPOW_OK, n, v);
   } else {
-    // "GPU returned invalid work": re-arm this device for the job after the slot retires
+    // "GPU returned invalid work": the launches that held this generation stopped at the win,
+    // so a bounded job gets back every range from the one holding the winner on; the job is
+    // re-armed on this device after the slot retires.  The third in a row drops the device.
     {
       std::lock_guard<std::mutex> sg(d_.stats_mu);
       d_.invalid++;
     }
     fprintf(stderr, "nanopow: GPU %d returned invalid work %016llx (value %016llx, cpu %016llx)\n", d_.id,
             (unsigned long long)n, (unsigned long long)v, (unsigned long long)cpu_v);
-    if (++j.invalid_streak[sl.k] >= 3)
-      j.err = "GPU " + std::to_string(d_.id) + " returned invalid work 3 consecutive times, abandoning it for this work";
-    else
-      sl.requeue = true;
+    if (j.max_per_dev) {
+      size_t from = 0;
+      for (size_t i = 0; i < sl.inflight.size(); ++i)
+        if (n - sl.inflight[i].base < sl.inflight[i].count) {
+          from = i;
+          break;
+        }
+      push_back_locked(sl, from);
+    }
+    sl.requeue = true;
+    if (++invalid_streak_ >= kInvalidStreakMax && !d_.dead) {
+      d_.dead_code = NPOW_ERR_INVALID_WORK;
+      d_.dead_msg = "GPU " + std::to_string(d_.id) + " returned invalid work " + std::to_string(kInvalidStreakMax) +
+                    " consecutive times";
+      d_.dead = true;
+      fprintf(stderr, "nanopow: %s, dropping it\n", d_.dead_msg.c_str());
+    }
   }
   sl.state = SlotState::kDraining;  // the winning wave already marked the slot dead on the device
+}
+
+// Ranges sl.inflight[from..] did not complete (their launches stopped on this generation or
+// failed): hand them back to the front of the job's queue for this device, in order.
+void Worker::push_back_locked(Slot& sl, size_t from) {
+  Job& j = *sl.job;
+  for (size_t i = sl.inflight.size(); i > from; --i)
+    j.todo[sl.k].push_front({sl.inflight[i - 1].base, sl.inflight[i - 1].count});
+  sl.inflight.resize(from);
+}
+
+// The launch's in-kernel clock records (PoolClk, one per XCD) into the device statistics.
+void Worker::account_clock(int ring, uint64_t seq) {
+  double cyc = 0, ref = 0;
+  for (int x = 0; x < kClkWaves; ++x) {
+    const PoolClk& c = d_.pmb->clk[ring][x];
+    if (__atomic_load_n(&c.seq, __ATOMIC_ACQUIRE) != (uint32_t)seq) continue;
+    cyc += (double)__atomic_load_n(&c.cycles, __ATOMIC_RELAXED);
+    ref += (double)__atomic_load_n(&c.ref, __ATOMIC_RELAXED);
+  }
+  std::lock_guard<std::mutex> sg(d_.stats_mu);
+  d_.clk_ticks += cyc;
+  d_.clk_ref_ticks += ref;
 }
 
 bool Worker::win_published(int s) const {
@@ -333,7 +476,10 @@ void Worker::check_slots() {
     }
     if (sl.state != SlotState::kActive) continue;
     Job& j = *sl.job;
-    if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {
+    if (d_.dead) {  // dropped device: stop every job's waves; retire() re-strides them
+      __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);
+      sl.state = SlotState::kDraining;
+    } else if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {
       if (!j.decided.load()) {
         std::lock_guard<std::mutex> g(g_pool.mu);
         j.cancel_req = true;
@@ -348,7 +494,7 @@ void Worker::check_slots() {
 }
 
 int Worker::launch() {
-  if (q_.size() >= 2) return NPOW_OK;
+  if (q_.size() >= 2 || d_.dead) return NPOW_OK;
   // The second launch in flight only has to be queued before the running one ends (its budget
   // is known): queued early, it would sit behind a launch that a win ends, and the job could
   // only be retired after it too had started and drained (~20 us of every search's latency).
@@ -371,6 +517,8 @@ int Worker::launch() {
   t.budget = g_budget_us.load() * 100u;  // s_memrealtime runs at 100 MHz
   t.yield_base = __atomic_load_n(&d_.pmb->yield, __ATOMIC_ACQUIRE);
   ++seq_;
+  t.ring = (uint32_t)ring_;
+  t.seq = (uint32_t)seq_;
   {
     std::lock_guard<std::mutex> g(g_pool.mu);  // issued[] is shared with other workers' reads
     for (uint32_t e = 0; e < n; ++e) {
@@ -381,20 +529,28 @@ int Worker::launch() {
       pe.threshold = j.threshold;
       pe.gen = sl.gen;
       pe.slot = (uint32_t)idx[e];
-      uint64_t& issued = j.issued[sl.k];
-      pe.base = j.start + sl.k * j.spacing + issued;
-      if (j.max_per_dev) {
-        const uint64_t own = (uint64_t)(W / n + (e < W % n ? 1u : 0u)) * iters * 64;
-        pe.count = std::min(own, j.max_per_dev - issued);
-        pe.bounded = 1;
+      // the next part of the device's queue of ranges: a bounded job's own waves cover it
+      // densely; an unbounded job claims a full launch region (W * iters * 64, holes allowed)
+      // unless less than that is left, which then becomes a dense bounded entry too
+      std::deque<Range>& todo = j.todo[sl.k];
+      const uint64_t own = (uint64_t)(W / n + (e < W % n ? 1u : 0u)) * iters * 64;
+      const uint64_t full = (uint64_t)W * iters * 64;
+      if (todo.empty()) todo.push_back({j.start, 0});  // cannot happen (adopt / no_more); an empty entry
+      Range& r = todo.front();
+      const uint64_t want = j.max_per_dev ? own : full;
+      pe.base = r.base;
+      pe.count = std::min(want, r.count);
+      pe.bounded = (j.max_per_dev || pe.count < full) ? 1 : 0;
+      if (pe.bounded) {
+        pe.count = std::min(pe.count, own);
         bounded = true;
-      } else {
-        pe.count = (uint64_t)W * iters * 64;
-        pe.bounded = 0;
       }
-      issued += pe.count;
+      r.base += pe.count;
+      r.count -= pe.count;
+      if (r.count == 0) todo.pop_front();
+      sl.inflight.push_back({seq_, pe.base, pe.count});
       if (g_trace_lat && j.t_launch == 0) j.t_launch = now_us();
-      if (j.max_per_dev && issued >= j.max_per_dev) sl.no_more = true;
+      if (todo.empty()) sl.no_more = true;
       sl.fresh = false;
     }
   }
@@ -405,6 +561,8 @@ int Worker::launch() {
   // stream beside the running launch, joined by an event, cost 1.5-2 % of kernel throughput:
   // the copy is a blit kernel that competes with the running launch.)
   static const bool force_upload = getenv("NANOPOW_TABLE_UPLOAD") != nullptr;  // A/B switch
+  if (faults().hip_dev == d_.id && seq_ > faults().hip_after)  // NANOPOW_FAULT_HIP (tests)
+    return fail(NPOW_ERR_HIP, "injected launch failure (NANOPOW_FAULT_HIP)");
   if (n <= (uint32_t)kArgEntries && !force_upload) {  // the table rides in the kernel arguments
     HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
     HIPTRY(launch_pool_arg(pool_grid_of(d_), d_.stream, t, bounded, d_.pst, d_.pmb_dev));
@@ -443,6 +601,18 @@ int Worker::retire() {
     if (e == hipErrorNotReady) break;
     if (e != hipSuccess) return fail(NPOW_ERR_HIP, std::string("pool launch: ") + hipGetErrorString(e));
     account_launch(d_, q_.front().ring);
+    account_clock(q_.front().ring, q_.front().seq);
+    // The launch's ranges are complete, except those of a generation that won in it (or in an
+    // earlier launch still unseen): handle such wins first, they hand back what did not finish.
+    const uint64_t seq = q_.front().seq;
+    for (int s = 0; s < kMaxSlots; ++s) {
+      Slot& sl = slots_[s];
+      if (sl.state == SlotState::kFree || sl.inflight.empty()) continue;
+      if (win_published(s)) handle_win(s);
+      size_t m = 0;
+      while (m < sl.inflight.size() && sl.inflight[m].seq <= seq) ++m;
+      sl.inflight.erase(sl.inflight.begin(), sl.inflight.begin() + (ptrdiff_t)m);
+    }
     if (g_trace_lat)
       for (Slot& sl : slots_)
         if (sl.state == SlotState::kDraining && sl.job && sl.job->t_win != 0 && sl.job->t_kend == 0)
@@ -474,7 +644,9 @@ int Worker::retire() {
       std::lock_guard<std::mutex> g(g_pool.mu);
       Job& j = *sl.job;
       j.done += delta;
-      if (sl.requeue && !j.decided && j.err.empty()) {
+      if (d_.dead) {
+        abandon_locked(sl.job, sl.k, d_.dead_code, d_.dead_msg);  // survivors take what is left
+      } else if (!j.decided && (sl.requeue || !j.todo[sl.k].empty())) {
         j.on_dev[sl.k] = 0;  // adopt() picks it up again with a fresh generation
         g_pool.version.fetch_add(1);
       } else {
@@ -487,15 +659,22 @@ int Worker::retire() {
   return NPOW_OK;
 }
 
+// A HIP call failed: the device is dropped at once (no draining: its queue cannot be trusted).
+// Ranges of launches that had not completed go back to their jobs, which re-stride them.
 void Worker::fail_all(const std::string& msg) {
-  d_.dead = true;
-  fprintf(stderr, "nanopow: device %d failed: %s\n", d_.id, msg.c_str());
+  fprintf(stderr, "nanopow: device %d failed: %s; dropping it\n", d_.id, msg.c_str());
   std::lock_guard<std::mutex> g(g_pool.mu);
+  if (!d_.dead) {
+    d_.dead_code = NPOW_ERR_HIP;
+    d_.dead_msg = "device " + std::to_string(d_.id) + " failed: " + msg;
+    d_.dead = true;
+  }
   for (Slot& sl : slots_) {
     if (sl.state == SlotState::kFree) continue;
-    if (sl.job->err.empty()) sl.job->err = msg;
-    device_done_locked(sl.job, sl.k);
+    if (sl.job->max_per_dev) push_back_locked(sl, 0);
+    abandon_locked(sl.job, sl.k, d_.dead_code, d_.dead_msg);
     sl.job.reset();
+    sl.inflight.clear();
     sl.state = SlotState::kFree;
   }
   q_.clear();
@@ -512,18 +691,21 @@ int Worker::step() {
 }
 
 void Worker::run() {
-  if (hipSetDevice(d_.hip_id) != hipSuccess) d_.dead = true;
+  prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // nap(): 1-us timer slack instead of the default 50 us
+  if (hipSetDevice(d_.hip_id) != hipSuccess) {
+    d_.dead_code = NPOW_ERR_HIP;
+    d_.dead_msg = "device " + std::to_string(d_.id) + ": hipSetDevice failed";
+    d_.dead = true;
+  }
   for (;;) {
     if (g_exiting.load(std::memory_order_relaxed)) return;
-    if (d_.dead) {
-      // a failed device only releases the jobs that name it
+    if (d_.dead && !busy()) {
+      // a dropped device (drained) hands every job that still names it to that job's survivors
+      if (dev_lock_.owns_lock()) dev_lock_.unlock();
       std::unique_lock<std::mutex> lk(g_pool.mu);
       for (const JobP& j : std::vector<JobP>(g_pool.active)) {
         const int k = index_in(*j, d_.id);
-        if (k >= 0 && !j->dev_done[k]) {
-          if (j->err.empty()) j->err = "device " + std::to_string(d_.id) + " failed";
-          device_done_locked(j, (size_t)k);
-        }
+        if (k >= 0 && !j->dev_done[k]) abandon_locked(j, (size_t)k, d_.dead_code, d_.dead_msg);
       }
       if (!g_pool.running) return;
       g_pool.cv_work.wait(lk);
@@ -566,8 +748,41 @@ void Worker::run() {
       if (dev_lock_.owns_lock()) dev_lock_.unlock();
       continue;
     }
-    cpu_relax();
+    nap();
   }
+}
+
+// Between two steps.  While a launch runs there is nothing to do until a win is published, a
+// job is decided or cancelled, new jobs arrive (they notify cv_work) or the next launch must be
+// queued: poll without sleeping only during the first kFreshSpinUs of a launch (wins at receive
+// difficulty come that early) and near the next launch's queueing point; otherwise sleep up to
+// g_poll_us on cv_work.  A win is then seen within ~g_poll_us (~0.25 % of a send-difficulty
+// search at 100 us) and the thread uses a few % of a core instead of all of it.
+void Worker::nap() {
+  if (g_poll_us <= 0 || q_.empty() || d_.dead || d_.tasks_waiting.load() > 0) {
+    cpu_relax();
+    return;
+  }
+  const double since = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - front_start_).count();
+  if (since < kFreshSpinUs) {
+    cpu_relax();
+    return;
+  }
+  double us = g_poll_us;
+  const double budget = (double)g_budget_us.load();
+  if (q_.size() == 1 && budget > 0) {
+    const double until_prelaunch = budget - kPrelaunchUs - since;
+    if (until_prelaunch <= 0) {
+      cpu_relax();
+      return;
+    }
+    us = std::min(us, until_prelaunch);
+  }
+  const uint64_t v = seen_version_;
+  std::unique_lock<std::mutex> lk(g_pool.mu);
+  g_pool.cv_work.wait_for(lk, std::chrono::duration<double, std::micro>(us), [&] {
+    return g_pool.version.load(std::memory_order_relaxed) != v || !g_pool.running || d_.tasks_waiting.load() > 0;
+  });
 }
 
 }  // namespace
@@ -597,15 +812,16 @@ int pool_device_init(Device& d) {
   return NPOW_OK;
 }
 
-void pool_device_free(Device& d) {
-  (void)hipFree(d.pst);
-  (void)hipHostFree(d.pmb);
+void pool_device_free(Device& d) {  // tolerates a partial pool_device_init
+  if (d.pst) (void)hipFree(d.pst);
+  if (d.pmb) (void)hipHostFree(d.pmb);
   for (int r = 0; r < kEventRing; ++r) {
-    (void)hipFree(d.d_tab[r]);
-    (void)hipHostFree(d.h_tab[r]);
+    if (d.d_tab[r]) (void)hipFree(d.d_tab[r]);
+    if (d.h_tab[r]) (void)hipHostFree(d.h_tab[r]);
   }
-  (void)hipHostFree(d.h_done);
-  for (int s = 0; s < kMaxSlots; ++s) (void)hipEventDestroy(d.ev_done[s]);
+  if (d.h_done) (void)hipHostFree(d.h_done);
+  for (int s = 0; s < kMaxSlots; ++s)
+    if (d.ev_done[s]) (void)hipEventDestroy(d.ev_done[s]);
 }
 
 void pool_start() {
@@ -646,9 +862,9 @@ void pool_stop() {
       j->finished = true;
     }
   }
+  for (auto& kv : g_pool.tickets) kv.second->cv.notify_all();
   g_pool.waiting.clear();
   g_pool.active.clear();
-  g_pool.cv_done.notify_all();
 }
 
 // -- jobs -------------------------------------------------------------------------------------------
@@ -666,11 +882,15 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   const uint64_t G = devs.size();
   j->spacing = G > 1 ? (~0ull / G) + 1 : 0;  // 2^64 / G (exact for powers of two)
   for (Device* d : devs) j->devs.push_back(d->id);
-  j->issued.assign(G, 0);
+  j->todo.resize(G);
+  for (uint64_t k = 0; k < G; ++k) {
+    // bounded: max_nonces_per_device; unbounded: the whole stride (2^64 / G; 2^64 - 1 with one device)
+    const uint64_t cnt = max_nonces_per_device ? max_nonces_per_device : (G > 1 ? j->spacing : ~0ull);
+    j->todo[k].push_back({start + k * j->spacing, cnt});
+  }
   j->on_dev.assign(G, 0);
   j->seen_dev.assign(G, 0);
   j->dev_done.assign(G, 0);
-  j->invalid_streak.assign(G, 0);
   j->pending_devs = (int)G;
   if (g_trace_lat) j->t_submit = now_us();
   std::lock_guard<std::mutex> g(g_pool.mu);
@@ -690,19 +910,23 @@ int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* va
   JobP j = it->second;
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us < 0 ? 0 : timeout_us);
   while (!j->finished) {
-    // a queued job's cancel word is polled here (active ones by the device workers)
+    // A queued job's cancel word is polled here, every 2 ms (admitted ones are polled by the
+    // device workers, and their waiters sleep until the job's own end).
     if (!j->admitted && j->cancel_seen()) {
       j->cancel_req = true;
       decide_locked(*j, NPOW_CANCELLED);
       finish_locked(j);
       break;
     }
-    auto wake = std::chrono::steady_clock::now() + std::chrono::microseconds(500);
-    if (timeout_us >= 0) {
-      if (std::chrono::steady_clock::now() >= deadline) return NPOW_PENDING;
-      wake = std::min(wake, deadline);
+    const auto now = std::chrono::steady_clock::now();
+    if (timeout_us >= 0 && now >= deadline) return NPOW_PENDING;
+    if (j->admitted && timeout_us < 0) {
+      j->cv.wait(lk);
+    } else {
+      auto wake = j->admitted ? deadline : now + std::chrono::microseconds(2000);
+      if (timeout_us >= 0) wake = std::min(wake, deadline);
+      j->cv.wait_until(lk, wake);
     }
-    g_pool.cv_done.wait_until(lk, wake);
   }
   if (nonces_done) *nonces_done = j->done;
   if (g_trace_lat)

@@ -57,7 +57,19 @@ class DeviceStats(ctypes.Structure):
         ("invalid_work", ctypes.c_uint64),
         ("cus", ctypes.c_int32),
         ("grid", ctypes.c_int32),
+        ("clock_mhz", ctypes.c_double),
+        ("host_cpu_ms", ctypes.c_double),
+        ("host_wall_ms", ctypes.c_double),
+        ("dead", ctypes.c_int32),
+        ("reserved", ctypes.c_int32),
     ]
+
+
+@dataclass
+class SweepResult:
+    status: int            # NPOW_OK, or NPOW_CANCELLED (hits then holds what was found before it)
+    hits: List[int]        # ascending (nonce - start); at most cap of them
+    total: int             # exact number of hits (may exceed len(hits) only with status != OK)
 
 
 @dataclass
@@ -284,15 +296,26 @@ class Engine:
                 out.append(SearchResult(status[i], None, None, 0))
         return out, done.value
 
-    def sweep(self, root: bytes, threshold: int, start: int, count: int, device_mask: int = 0,
-              cap: int = 1 << 16, cancel: Optional[CancelToken] = None) -> List[int]:
+    def sweep_result(self, root: bytes, threshold: int, start: int, count: int, device_mask: int = 0,
+                     cap: int = 1 << 16, cancel: Optional[CancelToken] = None) -> SweepResult:
+        """npow_sweep with its status: a cancelled sweep returns status NPOW_CANCELLED and the
+        hits found so far, never mistakable for the exact hit set of the range."""
         out = (ctypes.c_uint64 * max(cap, 1))()
         n = ctypes.c_uint64(0)
         rc = self.lib.npow_sweep(_root(root), threshold & M64, start & M64, count, device_mask,
                                  cancel.address if cancel else None, ctypes.addressof(out), cap,
                                  ctypes.byref(n))
         _check(rc, self.lib, ok=(NPOW_OK, NPOW_CANCELLED))
-        return list(out[: min(n.value, cap)])
+        return SweepResult(rc, list(out[: min(n.value, cap)]), n.value)
+
+    def sweep(self, root: bytes, threshold: int, start: int, count: int, device_mask: int = 0,
+              cap: int = 1 << 16, cancel: Optional[CancelToken] = None) -> List[int]:
+        """Every hit of [start, start + count) (exact).  Raises NanoPowError(NPOW_CANCELLED) if
+        `cancel` stopped it (sweep_result() returns the partial hits with the status)."""
+        r = self.sweep_result(root, threshold, start, count, device_mask, cap, cancel)
+        if r.status != NPOW_OK:
+            raise NanoPowError(r.status, f"sweep cancelled after {r.total} hits: the hit set is partial")
+        return r.hits
 
     def values(self, root: bytes, start: int, count: int, device: int = 0) -> List[int]:
         out = (ctypes.c_uint64 * max(count, 1))()
@@ -301,6 +324,8 @@ class Engine:
 
     def values_pairs(self, roots: Sequence[bytes], nonces: Sequence[int], device: int = 0) -> List[int]:
         n = len(nonces)
+        if len(roots) != n:  # the library reads n * 32 root bytes
+            raise ValueError(f"{len(roots)} roots for {n} nonces")
         rb = b"".join(_root(r) for r in roots)
         nn = (ctypes.c_uint64 * max(n, 1))(*[x & M64 for x in nonces])
         out = (ctypes.c_uint64 * max(n, 1))()

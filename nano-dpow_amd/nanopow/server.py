@@ -26,6 +26,8 @@ requests are handed to libnanopow's work pool at once (npow_submit), where
 every selected GPU searches all of them in the same kernel launches, so a
 burst of requests from many clients keeps the GPUs busy across request
 boundaries.  ``max_active=1`` is the reference's strictly serial service.
+Each connection's thread hands its own request to the engine and blocks there
+for the result (no dispatcher or per-request threads).
 Every reply a search produces was re-validated on the CPU inside libnanopow
 before it reaches this layer.
 """
@@ -35,15 +37,18 @@ import json
 import logging
 import os
 import random
+import socket
+import socketserver
 import threading
 import time
-from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional, Protocol
 
 from . import work as W
 from ._lib import NPOW_CANCELLED, NPOW_OK, CancelToken, NanoPowError, SearchResult
 
 log = logging.getLogger("nanopow.server")
+
+GENERATION_FAILED = {"error": "Work generation failed (see logs for details)"}
 
 
 class SearchTicket(Protocol):
@@ -60,7 +65,8 @@ class SearchEngine(Protocol):
 
 
 class Job:
-    __slots__ = ("root", "threshold", "cancel", "done", "reply", "active", "t_queued", "waiters", "t_started")
+    __slots__ = ("root", "threshold", "cancel", "done", "reply", "active", "t_queued", "waiters", "t_started",
+                 "ticket", "dispatched", "collector")
 
     def __init__(self, root: bytes, threshold: int) -> None:
         self.root = root
@@ -72,15 +78,24 @@ class Job:
         self.t_queued = time.perf_counter()
         self.t_started = 0.0
         self.waiters = 1
+        self.ticket: Optional[SearchTicket] = None
+        self.dispatched = threading.Event()  # ticket set, or the job already resolved
+        self.collector = False               # a request thread is collecting the ticket's result
 
     def resolve(self, reply: Dict[str, Any]) -> None:
         if not self.done.is_set():
             self.reply = reply
             self.done.set()
+        self.dispatched.set()
 
 
 class WorkServer:
-    """Request dispatcher: a FIFO (or shuffled) queue in front of the engine's work pool."""
+    """Request dispatcher: a FIFO (or shuffled) queue in front of the engine's work pool.
+
+    No thread of its own: a request is handed to the engine (npow_submit) by the request thread
+    that queued it when fewer than max_active are in flight, otherwise by the request thread whose
+    search ends next; each request thread then blocks in the engine (npow_wait, GIL released)
+    for its own result.  A request costs no thread hand-off on the way in or out."""
 
     def __init__(self, engine: SearchEngine, base_threshold: int = W.DEFAULT_BASE, shuffle: bool = False,
                  device_mask: int = 0, rng: Optional[random.Random] = None, max_active: int = 4) -> None:
@@ -96,16 +111,11 @@ class WorkServer:
         self._queue: List[Job] = []
         self._inflight: List[Job] = []
         self._running = False
-        self._dispatcher: Optional[threading.Thread] = None
 
     # -- lifecycle ---------------------------------------------------------------------
     def start(self) -> "WorkServer":
         with self._lock:
-            if self._running:
-                return self
             self._running = True
-        self._dispatcher = threading.Thread(target=self._dispatch_loop, name="nanopow-dispatch", daemon=True)
-        self._dispatcher.start()
         return self
 
     def stop(self) -> None:
@@ -118,14 +128,21 @@ class WorkServer:
             self._lock.notify_all()
         for j in pending:
             j.resolve({"error": "Cancelled"})
-        if self._dispatcher is not None:
-            self._dispatcher.join(timeout=10)
         deadline = time.time() + 10
         with self._lock:
             while self._inflight and time.time() < deadline:
                 self._lock.wait(0.1)
 
     # -- dispatch ----------------------------------------------------------------------
+    def handle_body(self, raw: bytes) -> Dict[str, Any]:
+        try:
+            req = json.loads(raw.decode("utf-8")) if raw else None
+        except (UnicodeDecodeError, json.JSONDecodeError):
+            req = None
+        if req is None:
+            return {"error": "Failed to deserialize JSON"}
+        return self.handle(req)
+
     def handle(self, req: Any) -> Dict[str, Any]:
         if not isinstance(req, dict):
             return {"error": "Failed to deserialize JSON"}
@@ -148,9 +165,7 @@ class WorkServer:
     def work_generate(self, req: Dict[str, Any]) -> Dict[str, Any]:
         root = W.parse_hash(req)
         threshold = W.requested_threshold(req, self.base)
-        job = self._enqueue(root, threshold)
-        job.done.wait()
-        return dict(job.reply)
+        return self._result(self._enqueue(root, threshold))
 
     def work_cancel(self, req: Dict[str, Any]) -> Dict[str, Any]:
         root = W.parse_hash(req)
@@ -193,9 +208,8 @@ class WorkServer:
                  W.fmt_multiplier(W.to_multiplier(threshold, self.base)))
         t0 = time.perf_counter()
         for _ in range(count):
-            job = self._enqueue(self.rng.getrandbits(256).to_bytes(32, "little"), threshold)
-            job.done.wait()
-            if "work" not in job.reply:
+            reply = self._result(self._enqueue(self.rng.getrandbits(256).to_bytes(32, "little"), threshold))
+            if "work" not in reply:
                 return {"error": "Benchmark failed", "hint": "Work generation failure"}
         ms = (time.perf_counter() - t0) * 1000.0
         return {"count": str(count), "difficulty": W.fmt_u64(threshold),
@@ -203,12 +217,12 @@ class WorkServer:
                 "duration": str(int(round(ms))), "average": str(int(round(ms / count))),
                 "hint": "Times in milliseconds"}
 
-    # -- queue + worker ----------------------------------------------------------------
+    # -- queue -------------------------------------------------------------------------
     def _enqueue(self, root: bytes, threshold: int) -> Job:
         with self._lock:
             if not self._running:
                 j = Job(root, threshold)
-                j.resolve({"error": "Work generation failed (see logs for details)"})
+                j.resolve(dict(GENERATION_FAILED))
                 return j
             # the same root at the same threshold queued or running: share its result
             for j in self._inflight + self._queue:
@@ -217,112 +231,180 @@ class WorkServer:
                     return j
             job = Job(root, threshold)
             self._queue.append(job)
-            self._lock.notify_all()
-            return job
+            ready = self._pump_locked()
+        self._submit(ready)
+        return job
 
-    def _next_job(self) -> Optional[Job]:
-        with self._lock:
-            while self._running and (not self._queue or len(self._inflight) >= self.max_active):
-                self._lock.wait()
-            if not self._running:
-                return None
+    def _pump_locked(self) -> List[Job]:
+        """Move queued jobs in flight while fewer than max_active are (FIFO, or a random one
+        with --shuffle); the caller submits them once the lock is released."""
+        ready = []
+        while self._running and self._queue and len(self._inflight) < self.max_active:
             idx = self.rng.randrange(len(self._queue)) if self.shuffle else 0
             job = self._queue.pop(idx)
             job.active = True
-            self._inflight.append(job)
-            return job
-
-    def _dispatch_loop(self) -> None:
-        while True:
-            job = self._next_job()
-            if job is None:
-                return
             job.t_started = time.perf_counter()
+            self._inflight.append(job)
+            ready.append(job)
+        return ready
+
+    def _submit(self, jobs: List[Job]) -> None:
+        for job in jobs:
             try:
-                ticket = self.engine.submit(job.root, job.threshold, start=self.rng.getrandbits(64),
-                                            device_mask=self.device_mask, cancel=job.cancel)
+                job.ticket = self.engine.submit(job.root, job.threshold, start=self.rng.getrandbits(64),
+                                                device_mask=self.device_mask, cancel=job.cancel)
             except Exception as e:  # never leave a client waiting
                 log.error("Error computing work: %s", e)
-                self._complete(job, {"error": "Work generation failed (see logs for details)"})
+                self._complete(job, dict(GENERATION_FAILED))
                 continue
-            threading.Thread(target=self._await, args=(job, ticket), name="nanopow-await", daemon=True).start()
+            job.dispatched.set()
 
-    def _await(self, job: Job, ticket: SearchTicket) -> None:
+    def _result(self, job: Job) -> Dict[str, Any]:
+        """Block until the job's reply exists; the first request thread to get here after the
+        job is in flight collects it from the engine, any other (a duplicate request) waits."""
+        job.dispatched.wait()
+        with self._lock:
+            mine = not job.done.is_set() and job.ticket is not None and not job.collector
+            if mine:
+                job.collector = True
+        if mine:
+            self._complete(job, self._collect(job))
+        job.done.wait()
+        return dict(job.reply)
+
+    def _collect(self, job: Job) -> Dict[str, Any]:
         try:
-            res = ticket.wait()
+            res = job.ticket.wait()
             if res is not None and res.status == NPOW_OK:
-                reply = {"work": W.fmt_u64(res.nonce), "difficulty": W.fmt_u64(res.value),
-                         "multiplier": W.fmt_multiplier(W.to_multiplier(res.value, self.base))}
                 log.info("Generated for %s in %.0fms for difficulty %016x", job.root.hex().upper(),
                          (time.perf_counter() - job.t_started) * 1000.0, job.threshold)
-            elif res is not None and res.status == NPOW_CANCELLED:
-                reply = {"error": "Cancelled"}
-            else:
-                reply = {"error": "Work generation failed (see logs for details)"}
+                return {"work": W.fmt_u64(res.nonce), "difficulty": W.fmt_u64(res.value),
+                        "multiplier": W.fmt_multiplier(W.to_multiplier(res.value, self.base))}
+            if res is not None and res.status == NPOW_CANCELLED:
+                return {"error": "Cancelled"}
+            return dict(GENERATION_FAILED)
         except NanoPowError as e:
             log.error("Error computing work: %s", e)
-            reply = {"error": "Work generation failed (see logs for details)"}
         except Exception as e:  # never leave a client waiting
             log.exception("work loop failure: %s", e)
-            reply = {"error": "Work generation failed (see logs for details)"}
-        self._complete(job, reply)
+        return dict(GENERATION_FAILED)
 
     def _complete(self, job: Job, reply: Dict[str, Any]) -> None:
         job.resolve(reply)
         with self._lock:
             if job in self._inflight:
                 self._inflight.remove(job)
+            ready = self._pump_locked()
             self._lock.notify_all()
+        self._submit(ready)
 
 
 # ---------------------------------------------------------------------------------------
-class _Handler(BaseHTTPRequestHandler):
-    protocol_version = "HTTP/1.1"
-    server_version = "nanopow-work-server/0.1"
+_REASON = {200: "OK", 400: "Bad Request", 405: "Method Not Allowed", 413: "Payload Too Large"}
+_MAX_LINE = 65536
+_MAX_BODY = 1 << 20
+
+
+class _Connection(socketserver.StreamRequestHandler):
+    """One HTTP/1.1 client connection (keep-alive; the DPoW client's aiohttp session reuses it for
+    every work_generate, client/work_handler.py:98-108): request line, headers, a JSON body ->
+    one JSON reply written with ONE send (status line, headers and body together; TCP_NODELAY).
+    A minimal parser: no email.parser header objects, no per-request allocation beyond the body."""
+    disable_nagle_algorithm = True
     work_server: WorkServer  # set on the subclass
 
-    def log_message(self, fmt: str, *args: Any) -> None:  # route to logging
-        log.debug("%s - %s", self.address_string(), fmt % args)
+    def handle(self) -> None:
+        rfile = self.rfile
+        while True:
+            line = rfile.readline(_MAX_LINE + 1)
+            if not line:
+                return
+            if line in (b"\r\n", b"\n"):
+                continue  # stray blank lines between requests (RFC 9112 2.2)
+            parts = line.split()
+            if len(parts) != 3 or not parts[2].startswith(b"HTTP/1."):
+                self._send(400, {"error": "Bad request line"}, True)
+                return
+            method, version = parts[0], parts[2]
+            close = version == b"HTTP/1.0"
+            length, chunked = 0, False
+            while True:
+                h = rfile.readline(_MAX_LINE + 1)
+                if h in (b"\r\n", b"\n", b""):
+                    break
+                name, _, value = h.partition(b":")
+                name = name.strip().lower()
+                if name == b"content-length":
+                    try:
+                        length = int(value.strip())
+                    except ValueError:
+                        length = -1
+                elif name == b"connection":
+                    v = value.strip().lower()
+                    close = v == b"close" or (version == b"HTTP/1.0" and v != b"keep-alive")
+                elif name == b"transfer-encoding":
+                    chunked = b"chunked" in value.lower()
+                elif name == b"expect" and value.strip().lower() == b"100-continue":
+                    self.wfile.write(b"HTTP/1.1 100 Continue\r\n\r\n")
+            if length < 0 or length > _MAX_BODY:
+                self._send(413 if length > 0 else 400, {"error": "Bad Content-Length"}, True)
+                return
+            body = self._read_chunked() if chunked else (rfile.read(length) if length else b"")
+            if body is None:
+                self._send(400, {"error": "Bad chunked body"}, True)
+                return
+            if method == b"POST":
+                self._send(200, self.work_server.handle_body(body), close)
+            else:
+                self._send(405, {"error": "Can only POST requests"}, close)
+            if close:
+                return
 
-    def _send(self, code: int, obj: Dict[str, Any]) -> None:
-        body = json.dumps(obj).encode()
-        self.send_response(code)
-        self.send_header("Content-Type", "application/json")
-        self.send_header("Content-Length", str(len(body)))
-        self.end_headers()
-        self.wfile.write(body)
+    def _read_chunked(self) -> Optional[bytes]:
+        out = []
+        total = 0
+        while True:
+            size_line = self.rfile.readline(_MAX_LINE + 1)
+            try:
+                n = int(size_line.split(b";")[0].strip(), 16)
+            except ValueError:
+                return None
+            if n == 0:
+                while self.rfile.readline(_MAX_LINE + 1) not in (b"\r\n", b"\n", b""):
+                    pass  # trailers
+                return b"".join(out)
+            total += n
+            if total > _MAX_BODY:
+                return None
+            out.append(self.rfile.read(n))
+            self.rfile.readline(_MAX_LINE + 1)  # the chunk's CRLF
 
-    def do_POST(self) -> None:  # noqa: N802
-        n = int(self.headers.get("Content-Length") or 0)
-        raw = self.rfile.read(n) if n else b""
+    def _send(self, code: int, obj: Dict[str, Any], close: bool) -> None:
+        data = json.dumps(obj).encode()
+        head = (f"HTTP/1.1 {code} {_REASON.get(code, 'OK')}\r\nContent-Type: application/json\r\n"
+                f"Content-Length: {len(data)}\r\n{'Connection: close' + chr(13) + chr(10) if close else ''}\r\n")
         try:
-            req = json.loads(raw.decode("utf-8")) if raw else None
-        except (UnicodeDecodeError, json.JSONDecodeError):
-            req = None
-        if req is None:
-            self._send(200, {"error": "Failed to deserialize JSON"})
-            return
-        self._send(200, self.work_server.handle(req))
-
-    def do_GET(self) -> None:  # noqa: N802
-        self._send(405, {"error": "Can only POST requests"})
+            self.wfile.write(head.encode() + data)
+        except OSError:
+            pass  # the client went away; its request was answered as far as the server is concerned
 
 
-class _Listener(ThreadingHTTPServer):
+class _Listener(socketserver.ThreadingTCPServer):
     # socketserver's default listen backlog is 5: a burst of concurrent work_generate
     # connections (many clients, or one client's precache wave) would overflow it and wait
     # out TCP's 1-s SYN retry.
     request_queue_size = 1024
+    allow_reuse_address = True
+    daemon_threads = True
 
 
 class HttpWorkServer:
     """WorkServer behind a threaded HTTP/1.1 listener (one thread per connection)."""
 
     def __init__(self, work_server: WorkServer, host: str = "127.0.0.1", port: int = 7000) -> None:
-        handler = type("Handler", (_Handler,), {"work_server": work_server})
+        handler = type("Connection", (_Connection,), {"work_server": work_server})
         self.work_server = work_server
         self.httpd = _Listener((host, port), handler)
-        self.httpd.daemon_threads = True
         self._thread: Optional[threading.Thread] = None
 
     @property

@@ -9,6 +9,7 @@ The multiplier formulas are the DPoW server's (server/dpow_server.py:250-255,
 """
 from __future__ import annotations
 
+import re
 from typing import Any, Dict, Tuple
 
 M64 = (1 << 64) - 1
@@ -22,6 +23,9 @@ RECEIVE_THRESHOLD = 0xfffffe0000000000
 DEFAULT_BASE = SEND_THRESHOLD
 
 SUPPORTED = "Supported commands: work_generate, work_cancel, work_validate, benchmark, status"
+
+# 1..16 hex digits and nothing else: int(x, 16) alone also takes "-1", "+f", "0x1f", " ff", "f_f"
+_HEX64 = re.compile(r"[0-9a-fA-F]{1,16}")
 
 
 class RequestError(Exception):
@@ -68,24 +72,18 @@ def parse_work(req: Dict[str, Any]) -> int:
         raise RequestError("Bad work", "Work is empty. Expecting a hex string")
     if len(w) > 16:
         raise RequestError("Bad work", "Work is too long (should be 8 bytes)")
-    try:
-        return int(w, 16)
-    except ValueError:
-        raise RequestError("Bad work", "Expecting a hex string for work") from None
+    if not _HEX64.fullmatch(w):
+        raise RequestError("Bad work", "Expecting a hex string for work")
+    return int(w, 16)
 
 
 def parse_threshold(s: Any) -> int:
     if not isinstance(s, str):
         raise RequestError("Bad difficulty", "Expecting a hex string for difficulty")
-    try:
-        v = int(s, 16)
-    except ValueError:
-        raise RequestError("Bad difficulty",
-                           "Threshold not a valid unsigned long (u64). Example: 'ffffffc000000000'") from None
-    if v < 0 or v > M64 or s.strip() == "" or len(s) > 16 or s.startswith(("-", "+")):
+    if not _HEX64.fullmatch(s):
         raise RequestError("Bad difficulty",
                            "Threshold not a valid unsigned long (u64). Example: 'ffffffc000000000'")
-    return v
+    return int(s, 16)
 
 
 def parse_multiplier(x: Any) -> float:

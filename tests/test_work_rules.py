@@ -21,7 +21,7 @@ def test_threshold_parsing():
     assert W.parse_threshold("fffffff800000000") == W.SEND_THRESHOLD
     assert W.parse_threshold("FFFFFE0000000000") == W.RECEIVE_THRESHOLD
     assert W.parse_threshold("0") == 0
-    for bad in ["", "g", "-1", "1" * 17, 5]:
+    for bad in ["", "g", "-1", "1" * 17, 5, "+f", "0x1f", " ff", "ff ", "f_f", "0X10"]:
         with pytest.raises(W.RequestError):
             W.parse_threshold(bad)
 
@@ -36,7 +36,13 @@ def test_work_and_hash_parsing():
     assert W.parse_hash({"hash": "AB" * 32}) == b"\xab" * 32
     assert W.parse_work({"work": "62f05417dd3fb691"}) == 0x62f05417dd3fb691
     assert W.parse_work({"work": "1"}) == 1
+    assert W.parse_work({"work": "FFFFFFFFFFFFFFFF"}) == (1 << 64) - 1
     assert W.fmt_u64(1) == "0000000000000001"
+    # int(x, 16) alone would take these (a negative work value would then be masked and validated)
+    for bad in ["-1", "+f", "0x1f", " ff", "f_f", "ff\n", "１"]:
+        with pytest.raises(W.RequestError) as e:
+            W.parse_work({"work": bad})
+        assert e.value.error == "Bad work"
 
 
 def test_gpu_spec_and_cli():
