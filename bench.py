@@ -11,8 +11,10 @@ fffffff800000000, from start nonce LE64(blake2b(b"start" + LE64(i), 8))
 
 value = Gnonce/s over the whole job = nonces hashed by all ranks (including
 the rest of a chunk after each win) / max over ranks of the timed wall time.
-p50 / p99 time-to-work are per-search wall times at the C ABI (rank 0 reports
-the distribution over every rank's searches).
+p50_ttw_ms / max_ttw_ms describe the timed searches; after the timed region
+rank 0 times --latency-searches (default 1,000) more searches on R_0..R_999 at
+the C ABI for a real p50 / p99 of time-to-work (ttw_c_abi_ms), and 100
+work_generate requests over one keep-alive HTTP connection (http_ttw_ms).
 
 Multi-GPU (``torch.distributed.run``, one rank per GPU): every rank searches
 its own roots on its own GPU (disjoint work, no data-path collective); gloo on
@@ -23,10 +25,15 @@ roofline: the dominant kernel (npow_pool_kernel<false>) is int32-VALU bound.
 achieved = nonces hashed in kernel x 2232 int32 ops/nonce /
 kernel time, the kernel time measured by HIP events recorded on the stream the
 kernel runs on (libnanopow stats); peak = 256 CUs x 128 int32 lanes/clk
-(4 x SIMD-32) x 2.4 GHz = 78.6 Tops/s.
-cpu_baseline (rank 0, N=1 only): the oracle's C restatement of the same work
-value (oracle/blake2b_oracle.c, "port"), exhaustive scan of a bounded sample of
-R_0's nonce space on the host cores; hashlib single-core rate alongside.
+(4 x SIMD-32) x 2.4 GHz = 78.6 Tops/s.  frac_at_measured_sclk prices the same
+achieved rate against 256 x 128 x the in-kernel shader clock of the timed
+launches (s_memtime / s_memrealtime spans of one wave per XCD per launch,
+libnanopow stats clock_mhz).
+cpu_baseline (rank 0, N=1 only, run before the GPU is opened): the reference's
+CPU path, hashlib.blake2b(digest_size=8), on every granted host core
+(multiprocessing, disjoint ranges of R_0 from 2^40 at fffffff8, "reference");
+the oracle's C restatement on the same cores and hashlib on one core alongside,
+and the hashlib hit set checked against the C oracle's over the same range.
 
 Other BASELINE.json configurations (``--workload``; not the driver's default line):
   allgpus   one process, every visible GPU on ONE root at a time (first win across
@@ -102,30 +109,65 @@ def pct(xs, p):
     return xs[k]
 
 
-def cpu_baseline(seconds: float = 12.0):
-    """Oracle C restatement on the host cores (bounded sample) + hashlib single-core rate."""
+CHECK_THR = 0xfffff00000000000  # cpu_baseline: hits kept at this lower threshold for the parity cross-check
+
+
+def _hashlib_scan(job):
+    """The reference CPU path (hashlib.blake2b(digest_size=8), dpow_server.py:130 rule value >= d)
+    over nonces [start, start + count) of one root; returns (hits >= CHECK_THR, seconds)."""
+    root, start, count = job
+    b2 = hashlib.blake2b
+    hits = []
+    t = time.perf_counter()
+    for n in range(start, start + count):
+        if int.from_bytes(b2(n.to_bytes(8, "little") + root, digest_size=8).digest(), "little") >= CHECK_THR:
+            hits.append(n)
+    return hits, time.perf_counter() - t
+
+
+def granted_cores() -> int:
+    """Host cores this process may use: its affinity set, at most 16 (the GPU box grants a one-GPU
+    job 16 CPUs; os.cpu_count() there shows the whole machine)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        n = os.cpu_count() or 1
+    return max(1, min(16, n))
+
+
+def cpu_baseline(seconds: float = 10.0):
+    """The reference's CPU path on every granted host core: hashlib.blake2b(digest_size=8) in one
+    process per core over disjoint ranges of R_0 from 2^40 (a bounded exhaustive sample, ~`seconds`
+    of wall time).  Alongside: hashlib on one core, and the oracle's C restatement on the same cores
+    over the same range, whose hit set must equal hashlib's.  Runs before the GPU is opened (fork)."""
+    import multiprocessing
     sys.path.insert(0, os.path.join(HERE, "oracle"))
     import oracle  # test infrastructure: the CPU baseline leg only
     oracle.build()
-    threads = min(16, os.cpu_count() or 1)  # the GPU box grants this process 16 CPUs
+    cores = granted_cores()
     root = bench_root(0)
-    # calibrate on one thread, then size the sample for ~`seconds` on all threads
+    _, dt1 = _hashlib_scan((root, 0, 200_000))
+    rate1 = 200_000 / dt1
+    per = int(rate1 * seconds)
+    base = 1 << 40
+    with multiprocessing.get_context("fork").Pool(cores) as pool:
+        t = time.perf_counter()
+        parts = pool.map(_hashlib_scan, [(root, base + i * per, per) for i in range(cores)], chunksize=1)
+        wall = time.perf_counter() - t
+    total = cores * per
+    hl_hits = sorted(h for hits, _ in parts for h in hits)
     t = time.perf_counter()
-    oracle.sweep(root, SEND, 0, 1 << 20, threads=1)
-    rate1 = (1 << 20) / (time.perf_counter() - t)
-    count = int(rate1 * threads * seconds)
-    t = time.perf_counter()
-    hits = oracle.sweep(root, SEND, 1 << 40, count, threads=threads)
-    dt = time.perf_counter() - t
-    n = 200_000
-    t = time.perf_counter()
-    for i in range(n):
-        hashlib.blake2b((i).to_bytes(8, "little") + root, digest_size=8).digest()
-    hl = n / (time.perf_counter() - t)
-    return {"value": round(count / dt / 1e9, 6), "unit": "Gnonce/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/blake2b_oracle.c exhaustive sweep of {count} nonces of R_0 from 2^40 at "
-                      f"fffffff800000000 ({len(hits)} hits) on {threads} pthreads, {dt:.1f} s",
-            "hashlib_1core_gnps": round(hl / 1e9, 6)}
+    c_hits = oracle.sweep(root, CHECK_THR, base, total, threads=cores)
+    c_dt = time.perf_counter() - t
+    n_send = sum(1 for h in hl_hits if oracle.work_value(root, h) >= SEND)
+    return {"value": round(total / wall / 1e9, 6), "unit": "Gnonce/s", "cores": cores, "kind": "reference",
+            "sample": f"hashlib.blake2b(digest_size=8) in {cores} processes (one per granted host core), exhaustive "
+                      f"scan of {total} nonces of R_0 from 2^40 at fffffff800000000 ({n_send} hits; {len(hl_hits)} at "
+                      f"fffff00000000000), {wall:.1f} s",
+            "hashlib_1core_gnps": round(rate1 / 1e9, 6),
+            "port_gnps": round(total / c_dt / 1e9, 6),
+            "port": f"oracle/blake2b_oracle.c on {cores} pthreads over the same range, {c_dt:.1f} s",
+            "hits_equal_port": hl_hits == c_hits}
 
 
 class NodeQueue:
@@ -454,8 +496,11 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
                            "one-GPU ranks; disjoint roots, no collective)",
         },
         "p50_ttw_ms": round(pct(all_ttw, 50) * 1e3, 3),
-        "p99_ttw_ms": round(pct(all_ttw, 99) * 1e3, 3),
+        # a p99 needs ~100 samples: fewer (the driver's 20 timed steps) report the maximum as such
+        **({"p99_ttw_ms": round(pct(all_ttw, 99) * 1e3, 3)} if len(all_ttw) >= 100 else
+           {"max_ttw_ms": round(max(all_ttw) * 1e3, 3)}),
         "mean_ttw_ms": round(statistics.mean(all_ttw) * 1e3, 3),
+        "n_ttw": len(all_ttw),
         "gnps_per_gpu": round(gnps / world, 4),
         "roofline": {
             "bound": "valu",
@@ -834,30 +879,63 @@ def _hashlib_search(root: bytes, thr: int, start: int, limit: int):
     return limit, None
 
 
-def _http_ttw(eng, n):
-    """BASELINE config 2 at the JSON boundary: n work_generate requests at fffffff8 POSTed one
-    at a time to the HTTP work server on 127.0.0.1 (fresh roots past the timed ones); wall
-    time per POST -> reply, each reply re-validated through npow_work_value."""
+class KeepAliveClient:
+    """One persistent HTTP/1.1 connection to the work server, as the DPoW client's aiohttp session
+    keeps one for its serial work_generate loop (client/work_handler.py:98-108)."""
+
+    def __init__(self, address: str):
+        import http.client
+        host, port = address.rsplit(":", 1)
+        self.conn = http.client.HTTPConnection(host, int(port), timeout=120)
+
+    def post(self, obj):
+        self.conn.request("POST", "/", json.dumps(obj), {"Content-Type": "application/json"})
+        return json.loads(self.conn.getresponse().read())
+
+    def close(self):
+        self.conn.close()
+
+
+def _http_ttw(eng, n, thr=SEND, base=30_000_000, device_mask=1):
+    """A config at the JSON boundary: n work_generate requests POSTed one at a time over one
+    keep-alive connection to the HTTP work server on 127.0.0.1 (fresh roots); wall time per
+    POST -> reply, each reply re-validated through npow_work_value."""
     from nanopow.server import HttpWorkServer, WorkServer
-    import urllib.request
-    srv = HttpWorkServer(WorkServer(eng, max_active=1, device_mask=1), "127.0.0.1", 0).start()
+    srv = HttpWorkServer(WorkServer(eng, max_active=1, device_mask=device_mask), "127.0.0.1", 0).start()
+    cli = KeepAliveClient(srv.address)
     out = []
     try:
         for i in range(n):
-            root = bench_root(30_000_000 + i)
-            body = json.dumps({"action": "work_generate", "hash": root.hex().upper(),
-                               "difficulty": f"{SEND:016x}"}).encode()
+            root = bench_root(base + i)
             t = time.perf_counter()
-            req = urllib.request.Request(f"http://{srv.address}", data=body, method="POST",
-                                         headers={"Content-Type": "application/json"})
-            with urllib.request.urlopen(req, timeout=60) as resp:
-                rep = json.loads(resp.read())
+            rep = cli.post({"action": "work_generate", "hash": root.hex().upper(), "difficulty": f"{thr:016x}"})
             out.append(time.perf_counter() - t)
-            if eng.work_value(root, int(rep["work"], 16)) < SEND:
+            if eng.work_value(root, int(rep["work"], 16)) < thr:
                 raise RuntimeError(f"HTTP reply {rep} does not validate")
     finally:
+        cli.close()
         srv.stop()
     return out
+
+
+def latency_sample(eng, dev: int, n: int):
+    """BASELINE config 2's time-to-work on a real sample: n first-win searches on R_0..R_{n-1} at
+    fffffff8 through the C ABI, one at a time, after the timed region (not part of value)."""
+    ttw, nonces = [], 0
+    t0 = time.perf_counter()
+    for i in range(n):
+        t = time.perf_counter()
+        r = eng.search(bench_root(i), SEND, start=bench_start(i), device_mask=1 << dev)
+        ttw.append(time.perf_counter() - t)
+        if r.status != 0:
+            raise RuntimeError(f"latency search {i} returned status {r.status}")
+        nonces += r.nonces_done
+    wall = time.perf_counter() - t0
+    return {"p50": round(pct(ttw, 50) * 1e3, 3), "p99": round(pct(ttw, 99) * 1e3, 3),
+            "mean": round(statistics.mean(ttw) * 1e3, 3), "n": n, "gnps": round(nonces / wall / 1e9, 4),
+            "roots": f"R_0..R_{n - 1}",
+            "note": "npow_search at fffffff800000000 through the C ABI, one at a time, after the timed region; "
+                    "expected p50 = ln2 * 2^29 nonces / rate; not part of value"}
 
 
 def workload_receive(eng, args, rank, world, dist):
@@ -876,18 +954,20 @@ def workload_receive(eng, args, rank, world, dist):
         r = eng.search(bench_root(20_000_000 + i), recv, start=bench_start(i), device_mask=0)
         gpu.append(time.perf_counter() - t)
         assert r.status == 0 and r.value >= recv
-    # GPU through the HTTP work server (what the DPoW client sees)
+    # GPU through the HTTP work server (what the DPoW client sees): one keep-alive connection, as
+    # the client's aiohttp session, and a new connection per request
+    http = _http_ttw(eng, min(args.steps, 300), thr=recv, base=21_000_000, device_mask=0)
     srv = HttpWorkServer(WorkServer(eng, max_active=1), "127.0.0.1", 0).start()
-    http = []
+    http_new = []
     try:
         for i in range(min(args.steps, 100)):
-            body = json.dumps({"action": "work_generate", "hash": bench_root(21_000_000 + i).hex(),
+            body = json.dumps({"action": "work_generate", "hash": bench_root(23_000_000 + i).hex(),
                                "difficulty": f"{recv:016x}"}).encode()
             t = time.perf_counter()
             req = urllib.request.Request(f"http://{srv.address}", data=body, method="POST")
             with urllib.request.urlopen(req, timeout=60) as resp:
                 rep = json.loads(resp.read())
-            http.append(time.perf_counter() - t)
+            http_new.append(time.perf_counter() - t)
             assert "work" in rep
     finally:
         srv.stop()
@@ -917,7 +997,10 @@ def workload_receive(eng, args, rank, world, dist):
                       "threshold": "fffffe0000000000"}
     line["receive"] = {
         "gpu_c_abi_ms": {"p50": round(pct(gpu, 50) * 1e3, 3), "p99": round(pct(gpu, 99) * 1e3, 3), "n": len(gpu)},
-        "gpu_http_ms": {"p50": round(pct(http, 50) * 1e3, 3), "p99": round(pct(http, 99) * 1e3, 3), "n": len(http)},
+        "gpu_http_keepalive_ms": {"p50": round(pct(http, 50) * 1e3, 3), "p99": round(pct(http, 99) * 1e3, 3),
+                                  "n": len(http)},
+        "gpu_http_new_connection_ms": {"p50": round(pct(http_new, 50) * 1e3, 3),
+                                       "p99": round(pct(http_new, 99) * 1e3, 3), "n": len(http_new)},
         "cpu_hashlib_1core_ms": {"p50": round(pct(cpu1, 50) * 1e3, 1), "n": len(cpu1),
                                  "gnps": round(cpu1_nonces / sum(cpu1) / 1e9, 6)},
         "cpu_oracle_c_scan_2p24_ms": {"median": round(statistics.median(cpun) * 1e3, 1), "threads": threads,
@@ -950,7 +1033,14 @@ def main() -> int:
                     help="search, N>1: roots searched by all ranks at once after the timed steps (node time-to-work)")
     ap.add_argument("--http-requests", type=int, default=100,
                     help="search, N=1: work_generate requests timed at the JSON boundary after the timed steps")
+    ap.add_argument("--latency-searches", type=int, default=1000,
+                    help="search, N=1: C-ABI searches on R_0..R_{n-1} after the timed steps (p50/p99 time-to-work)")
     args = ap.parse_args()
+
+    # The CPU baseline runs first, before anything opens the GPU (its worker processes are forked).
+    cpu = None
+    if args.workload == "search" and WORLD == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline()
 
     rank = int(os.environ.get("RANK", "0"))
     dist = None
@@ -989,31 +1079,54 @@ def main() -> int:
             raise RuntimeError(f"search {i} returned status {r.status}")
         return dt, r.nonces_done
 
+    timed_stats = []
+
     def stats():
         st = eng.stats(dev)
+        timed_stats.append(st)  # read right after the timed region: its clock and host CPU too
         return st.kernel_ms, st.nonces, st.launches
 
     with SclkSampler(dev) as sclk:
         res = run_timed(search, stats, lambda: eng.reset_stats(dev), args.steps, args.warmup, rank, WORLD, dist)
+    st = timed_stats[-1]
+    local = (st.clock_mhz, st.host_cpu_ms / st.host_wall_ms if st.host_wall_ms > 0 else 0.0)
+    if dist is not None:
+        gathered = [None] * WORLD
+        dist.all_gather_object(gathered, local)
+    else:
+        gathered = [local]
+    lat = latency_sample(eng, dev, args.latency_searches) if (WORLD == 1 and args.latency_searches) else None
     http = _http_ttw(eng, args.http_requests) if (rank == 0 and WORLD == 1 and args.http_requests) else None
     node = None
     if dist is not None and args.node_searches > 0 and int(os.environ.get("LOCAL_WORLD_SIZE", WORLD)) == WORLD:
         node = node_time_to_work(eng, dev, rank, WORLD, dist, args.node_searches)
     if rank == 0:
         line = result_line(WORLD, args.steps, args.warmup, *res)
+        clocks = [g[0] for g in gathered if g[0] > 0]
+        if clocks:
+            mhz = statistics.mean(clocks)
+            line["sclk_mhz"] = {"mean": round(mhz, 1), "ranks": len(clocks),
+                                "source": "in-kernel: s_memtime / s_memrealtime spans of one wave per XCD in every "
+                                          "timed search launch (libnanopow stats clock_mhz), mean over ranks"}
+            line["roofline"]["frac_at_measured_sclk"] = round(line["roofline"]["achieved"] /
+                                                              (256 * 128 * mhz * 1e6 / 1e12), 4)
         clk = sclk.summary()
-        line["sclk_mhz"] = clk
         if clk:
-            peak_at_clk = 256 * 128 * clk["mean"] * 1e6 / 1e12
-            line["roofline"]["frac_at_measured_sclk"] = round(line["roofline"]["achieved"] / peak_at_clk, 4)
+            line["sysfs_sclk_mhz"] = clk
+        line["host_worker_cpu"] = {"max_core_share": round(max(g[1] for g in gathered), 4),
+                                   "what": "CPU time of the GPU's pool worker thread / wall time over the timed "
+                                           "searches (libnanopow stats host_cpu_ms / host_wall_ms), max over ranks"}
+        if lat:
+            line["ttw_c_abi_ms"] = lat
         if node:
             line["node_ttw_ms"] = node
         if http:
             line["http_ttw_ms"] = {"p50": round(pct(http, 50) * 1e3, 3), "p99": round(pct(http, 99) * 1e3, 3),
-                                   "n": len(http), "note": "POST work_generate -> reply at the JSON boundary "
-                                   "(127.0.0.1 HTTP work server), after the timed region; not part of value"}
-        if WORLD == 1 and not args.no_cpu_baseline:
-            line["cpu_baseline"] = cpu_baseline()
+                                   "n": len(http), "note": "POST work_generate -> reply over one keep-alive "
+                                   "connection to the 127.0.0.1 HTTP work server (as the DPoW client's aiohttp "
+                                   "session), after the timed region; not part of value"}
+        if cpu:
+            line["cpu_baseline"] = cpu
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

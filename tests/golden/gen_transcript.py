@@ -10,6 +10,14 @@ tests/test_server.py replays the transcript against nanopow's server and
 checks the replies satisfy what WorkHandler reads from them.
 
 Run: python3 tests/golden/gen_transcript.py   (needs /root/reference and aiohttp)
+
+``--live`` drives the same reference caller against THIS repository's work server instead of
+a recorder: nanopow.server.HttpWorkServer backed by the oracle stand-in engine
+(tests/fake_engine.py), through start() (the blocking `requests` probe), queue_work x N on the
+aiohttp keep-alive session, a duplicate queue_work, queue_cancel of a queued hash (popped
+locally, never sent) and of an in-flight hash (work_cancel on a second connection).  It writes
+tests/golden/workhandler_live.json: every request and reply in server order with the
+connection each came on, and every callback the client made.  tests/test_server.py checks it.
 """
 from __future__ import annotations
 
@@ -78,10 +86,103 @@ class Rec(BaseHTTPRequestHandler):
         self.wfile.write(data)
 
 
+def drive_live(mod) -> dict:
+    """The reference WorkHandler against nanopow's HttpWorkServer (oracle stand-in engine)."""
+    sys.path.insert(0, os.path.join(HERE, ".."))
+    sys.path.insert(0, os.path.join(HERE, "..", "..", "nano-dpow_amd"))
+    from fake_engine import OracleEngine
+    from nanopow.server import HttpWorkServer, WorkServer
+
+    rec, conns = [], {}
+    rec_lock = threading.Lock()
+    peer = threading.local()  # the client (port) of the connection this request thread serves
+
+    class RecordingWorkServer(WorkServer):
+        def handle(self, req):
+            with rec_lock:
+                conn = conns.setdefault(peer.port, len(conns))
+                entry = {"conn": conn, "request": req}
+                rec.append(entry)
+            reply = super().handle(req)
+            with rec_lock:
+                entry["reply"] = reply
+            return reply
+
+    srv = HttpWorkServer(RecordingWorkServer(OracleEngine(chunk=1 << 14), max_active=1), "127.0.0.1", 0)
+    conn_cls = srv.httpd.RequestHandlerClass
+
+    class PeerConnection(conn_cls):
+        def handle(self):
+            peer.port = self.client_address[1]
+            super().handle()
+    srv.httpd.RequestHandlerClass = PeerConnection
+    srv.start()
+    hashes = [hashlib.blake2b(b"live-%d" % i, digest_size=32).hexdigest().upper() for i in range(8)]
+    hold = hashlib.blake2b(b"live-hold", digest_size=32).hexdigest().upper()
+    queued = hashlib.blake2b(b"live-queued", digest_size=32).hexdigest().upper()
+    callbacks, errors = [], []
+
+    async def cb(client, work_type, block_hash, work):
+        callbacks.append({"work_type": work_type, "hash": block_hash, "work": work})
+
+    async def err_cb():
+        errors.append(True)
+
+    def requested(h):
+        with rec_lock:
+            return any(e["request"].get("hash") == h and e["request"].get("action") == "work_generate" for e in rec)
+
+    async def drive():
+        wh = mod.WorkHandler(srv.address, None, cb, err_cb)
+        await wh.start()                                   # blocking requests probe (own connection)
+        task = asyncio.ensure_future(wh.loop())
+        await wh.queue_work("precache", hold, "ffffffffffffffff")   # never completes on its own
+        for _ in range(200):
+            if requested(hold):
+                break
+            await asyncio.sleep(0.02)
+        await wh.queue_work("precache", hold, "ffffffffffffffff")   # duplicate of in-flight work: ignored
+        await wh.queue_work("ondemand", queued, DIFF)               # queued behind it in the client ...
+        await wh.queue_cancel(queued)                               # ... and cancelled there: never sent
+        await wh.queue_cancel(hold)                                 # in flight: work_cancel, 2nd connection
+        for i, h in enumerate(hashes):
+            await wh.queue_work("ondemand" if i % 2 == 0 else "precache", h, DIFF)
+        for _ in range(1000):
+            if len(callbacks) >= len(hashes):
+                break
+            await asyncio.sleep(0.02)
+        task.cancel()
+        await wh.stop()
+
+    try:
+        asyncio.new_event_loop().run_until_complete(drive())
+    finally:
+        srv.stop()
+    return {
+        "generator": "tests/golden/gen_transcript.py --live (reference client/work_handler.py driven against "
+                     "nanopow.server.HttpWorkServer with the oracle stand-in engine)",
+        "difficulty": DIFF, "hashes": hashes, "hold": hold, "queued_then_cancelled": queued,
+        "log": rec, "callbacks": callbacks, "error_callbacks": len(errors),
+        "notes": "conn = the client connection (source port, numbered in order of appearance) a request arrived on: the probe is a blocking `requests` "
+                 "POST (work_handler.py:53); work_generate / work_cancel go through the aiohttp session "
+                 "(:75-78, :104-108), which reuses a connection once a reply has been read (:115) and opens "
+                 "another while one is busy or left unread (the cancelled generate's reply is never read, :109-114).",
+    }
+
+
 def main() -> int:
     spec = importlib.util.spec_from_file_location("ref_work_handler", REF)
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
+    if "--live" in sys.argv[1:]:
+        out = drive_live(mod)
+        path = os.path.join(HERE, "workhandler_live.json")
+        with open(path, "w") as f:
+            json.dump(out, f, indent=1)
+            f.write("\n")
+        print(json.dumps({k: out[k] for k in ("callbacks", "error_callbacks")}, indent=1))
+        print(f"{len(out['log'])} requests -> {path}")
+        return 0
 
     httpd = ThreadingHTTPServer(("127.0.0.1", 0), Rec)
     httpd.daemon_threads = True

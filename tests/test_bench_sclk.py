@@ -30,3 +30,12 @@ def test_sampler_without_sysfs_reports_nothing():
     with s:
         pass
     assert s.summary() is None
+
+
+def test_cpu_baseline_is_hashlib_on_every_granted_core():
+    """cpu_baseline: hashlib (the reference CPU path) in one process per granted core over disjoint
+    ranges; its hit set equals the C oracle's over the same range."""
+    out = bench.cpu_baseline(seconds=0.3)
+    assert out["kind"] == "reference" and out["cores"] == bench.granted_cores()
+    assert out["value"] > 0 and out["port_gnps"] > out["value"] and out["hits_equal_port"]
+    assert "hashlib.blake2b(digest_size=8)" in out["sample"]

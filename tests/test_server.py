@@ -266,3 +266,37 @@ def test_burst_of_concurrent_connections_is_accepted_at_once():
     for i in range(n):
         assert oracle.work_value(bytes.fromhex(f"{i + 1:064X}"), int(out[i]["work"], 16)) >= 0x1000000000000000
     assert max(lat) < 0.9, sorted(lat)[-5:]
+
+
+def test_reference_workhandler_against_this_server():
+    """tests/golden/workhandler_live.json: the reference caller itself (client/work_handler.py:
+    start, queue_work, queue_cancel, loop) driven against nanopow.server.HttpWorkServer (oracle
+    stand-in engine) by gen_transcript.py --live.  Pins what that client did to this server:
+    the blocking `requests` probe on its own connection (:50-55), serial work_generate on the
+    aiohttp keep-alive session (:98-117), a duplicate queue_work ignored (:83-89), a queued hash
+    cancelled locally and never sent (:61-66), an in-flight one cancelled by work_cancel on a
+    second connection (:70-80) whose pending generate answered Cancelled with no callback."""
+    t = load_golden("workhandler_live.json")
+    log = t["log"]
+    probe = log[0]
+    assert probe["request"] == {"action": "invalid"} and probe["reply"]["error"] == "Unknown command"
+    assert all(e["conn"] != probe["conn"] for e in log[1:])  # requests closed its connection
+    session_conns = {e["conn"] for e in log[1:]}
+    assert len(session_conns) <= 2  # keep-alive: one connection, a second only while the first is busy
+    gens = [e for e in log if e["request"]["action"] == "work_generate"]
+    cancels = [e for e in log if e["request"]["action"] == "work_cancel"]
+    hold = [e for e in gens if e["request"]["hash"] == t["hold"]]
+    assert len(hold) == 1 and hold[0]["reply"] == {"error": "Cancelled"}
+    assert [c["request"] for c in cancels] == [{"action": "work_cancel", "hash": t["hold"]}]
+    assert cancels[0]["reply"] == {} and cancels[0]["conn"] != hold[0]["conn"]
+    assert all(e["request"].get("hash") != t["queued_then_cancelled"] for e in log)
+    by_hash = {e["request"]["hash"]: e for e in gens if e["request"]["hash"] != t["hold"]}
+    assert sorted(by_hash) == sorted(t["hashes"]) and len(gens) == len(t["hashes"]) + 1
+    thr = int(t["difficulty"], 16)
+    assert t["error_callbacks"] == 0 and len(t["callbacks"]) == len(t["hashes"])
+    for c in t["callbacks"]:
+        rep = by_hash[c["hash"]]["reply"]
+        assert c["work"] == rep["work"] and c["work_type"] == ("ondemand" if t["hashes"].index(c["hash"]) % 2 == 0
+                                                              else "precache")
+        v = oracle.work_value_hashlib(bytes.fromhex(c["hash"]), int(c["work"], 16))
+        assert v >= thr and int(rep["difficulty"], 16) == v
