@@ -5,7 +5,9 @@ launched as ``--gpu 0:0 -l 127.0.0.1:7000`` by client/run_windows.bat:27 and
 client/README.md:31):
 
   -l/--listen-address ADDR      default 127.0.0.1:7000 (the DPoW client's --worker_uri default)
-  -g/--gpu PLATFORM:DEVICE[:THREADS]   repeatable; PLATFORM is ignored (HIP has one)
+  -g/--gpu PLATFORM:DEVICE[:THREADS]   repeatable; PLATFORM is ignored (HIP has one); THREADS
+                                (nonces per launch in the reference, default 1048576) is a lower
+                                bound on a search launch's nonces (see apply_threads)
   -c/--cpu-threads N            rejected: this engine runs on MI355X GPUs only
   --gpu-local-work-size N       accepted and ignored (workgroups are 256 lanes on gfx950)
   --shuffle                     pick a random queued request instead of the oldest
@@ -44,6 +46,25 @@ def parse_args(argv=None) -> argparse.Namespace:
     return ap.parse_args(argv)
 
 
+def apply_threads(eng, gpus) -> int:
+    """Honour THREADS of ``--gpu P:D:THREADS``: the reference hashes THREADS nonces per kernel launch
+    (nano-work-server.exe @1681064).  Here a search launch hashes up to grid lanes x iterations
+    nonces and ends on a time budget, so THREADS is applied as a lower bound: the iteration cap
+    is raised until one launch can hold THREADS nonces (at most 65,536 iterations); below that
+    it changes nothing.  Returns the iteration cap in force (0 = left as it was)."""
+    iters = 0
+    for _platform, device, threads in gpus:
+        lanes = eng.stats(device).grid * 256
+        if lanes > 0:
+            iters = max(iters, -(-threads // lanes))
+    if iters > 8192:  # the engine's default cap: 2^31 nonces per launch on 256 CUs
+        iters = min(iters, 65536)
+        eng.set_tuning(iters, 0, 0)
+        logging.info("THREADS: search launches capped at %d wave iterations", iters)
+        return iters
+    return 0
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
     logging.basicConfig(level=logging.DEBUG if args.verbose else logging.INFO,
@@ -74,6 +95,7 @@ def main(argv=None) -> int:
     if not 1 <= args.max_active <= 64:
         print("--max-active must be in [1, 64]", file=sys.stderr)
         return 2
+    apply_threads(eng, gpus)
     srv = HttpWorkServer(WorkServer(eng, base_threshold=base, shuffle=args.shuffle, device_mask=mask,
                                     max_active=args.max_active), host, port_i)
     logging.info("Configured for the live network with threshold %016x", base)

@@ -392,8 +392,9 @@ class _Connection(socketserver.StreamRequestHandler):
 class _Listener(socketserver.ThreadingTCPServer):
     # socketserver's default listen backlog is 5: a burst of concurrent work_generate
     # connections (many clients, or one client's precache wave) would overflow it and wait
-    # out TCP's 1-s SYN retry.
-    request_queue_size = 1024
+    # out TCP's 1-s SYN retry, or be reset.  4,096 connections at once (BASELINE configs[3])
+    # overflowed 1,024 with resets; the kernel caps this at net.core.somaxconn.
+    request_queue_size = 8192
     allow_reuse_address = True
     daemon_threads = True
 

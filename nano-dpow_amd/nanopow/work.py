@@ -139,7 +139,7 @@ def parse_count(req: Dict[str, Any]) -> int:
 def parse_gpu_spec(spec: str) -> Tuple[int, int, int]:
     """``PLATFORM:DEVICE[:THREADS]`` (nano-work-server.exe @1681064).  HIP has a single
     platform, so PLATFORM is accepted and ignored; THREADS (nonces per launch,
-    default 1048576) becomes a lower bound on the launch chunk."""
+    default 1048576) becomes a lower bound on the launch chunk (__main__.apply_threads)."""
     parts = spec.split(":")
     if len(parts) not in (2, 3):
         raise ValueError(f"bad --gpu spec {spec!r}: expected PLATFORM:DEVICE[:THREADS]")

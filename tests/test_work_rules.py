@@ -58,3 +58,23 @@ def test_gpu_spec_and_cli():
 def test_cpu_threads_rejected():
     from nanopow.__main__ import main
     assert main(["--cpu-threads", "4"]) == 2
+
+
+def test_gpu_threads_is_a_lower_bound_on_the_launch():
+    """--gpu P:D:THREADS (nonces per launch in the reference, @1681064) raises the iteration cap
+    only when a launch could not hold THREADS nonces."""
+    from nanopow.__main__ import apply_threads
+
+    class Stub:
+        def __init__(self):
+            self.tuning = None
+
+        def stats(self, device):
+            return type("S", (), {"grid": 1024})()  # 256 CUs x 4 workgroups: 262,144 lanes
+
+        def set_tuning(self, iters, poll, blocks):
+            self.tuning = iters
+    e = Stub()
+    assert apply_threads(e, [(0, 0, 1048576)]) == 0 and e.tuning is None   # the default: 4 iterations' worth
+    assert apply_threads(e, [(0, 0, 1 << 32)]) == 16384 and e.tuning == 16384
+    assert apply_threads(e, [(0, 0, 1 << 40)]) == 65536                   # capped
