@@ -456,7 +456,7 @@ class SclkSampler:
                           f"{int(self.period * 1e3)} ms over the warmup and timed searches"}
 
 
-def _pmc_traffic(name="r01_pmc_pool.json"):
+def _pmc_traffic(name="r02_pmc_pool.json"):
     """HBM bytes per launch of the workload's dominant kernel measured by rocprofv3 PMC passes
     (tools/pmc_bench.sh on that workload; FETCH_SIZE doubled per the gfx950 correction).  PMC
     needs the profiler around the process, so the bench reports the committed measurement;
@@ -511,7 +511,7 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
             "frac": round(achieved / PEAK_TOPS, 4),
             "traffic": _pmc_traffic(),
             "traffic_unit": "HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
-                            "(profiles/r01_pmc_pool.json, tools/pmc_bench.sh); algorithmic bytes: 0",
+                            "(profiles/r02_pmc_pool.json, tools/pmc_bench.sh); algorithmic bytes: 0",
             "ops_per_nonce": OPS_PER_NONCE,
             "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
             "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
