@@ -26,7 +26,9 @@ import json
 import logging
 import random
 import time
-import urllib.request
+import http.client
+import threading
+import urllib.parse
 from typing import Awaitable, Callable, Dict, Optional, Tuple
 
 log = logging.getLogger("nanopow.dpow")
@@ -67,17 +69,39 @@ def result_message(work_type: str, block_hash: str, work: str, payout: str) -> T
 
 
 class HttpWorker:
-    """POSTs JSON actions to a work server (the WorkHandler's aiohttp session, work_handler.py:47-53)."""
+    """POSTs JSON actions to a work server over keep-alive HTTP/1.1 connections, as the
+    WorkHandler's aiohttp session does (work_handler.py:51, :75-78, :104-108): each executor thread
+    keeps one connection and reuses it; a request that finds its connection closed by the server
+    is sent once more on a fresh one."""
 
     def __init__(self, uri: str, timeout: float = 300.0) -> None:
         self.uri = uri if uri.startswith("http") else f"http://{uri}"
+        u = urllib.parse.urlsplit(self.uri)
+        self.host, self.port = u.hostname or "127.0.0.1", u.port or 80
+        self.path = u.path or "/"
         self.timeout = timeout
+        self._local = threading.local()
+
+    def _conn(self, fresh: bool = False) -> http.client.HTTPConnection:
+        c = getattr(self._local, "conn", None)
+        if c is None or fresh:
+            if c is not None:
+                c.close()
+            c = self._local.conn = http.client.HTTPConnection(self.host, self.port, timeout=self.timeout)
+        return c
 
     def _post(self, obj: Dict) -> Dict:
-        req = urllib.request.Request(self.uri, data=json.dumps(obj).encode(),
-                                     headers={"Content-Type": "application/json"}, method="POST")
-        with urllib.request.urlopen(req, timeout=self.timeout) as r:
-            return json.loads(r.read())
+        body = json.dumps(obj)
+        for attempt in (0, 1):
+            c = self._conn(fresh=attempt == 1)
+            try:
+                c.request("POST", self.path, body, {"Content-Type": "application/json"})
+                return json.loads(c.getresponse().read())
+            except (http.client.RemoteDisconnected, ConnectionResetError, BrokenPipeError,
+                    http.client.CannotSendRequest):
+                if attempt == 1:
+                    raise
+        raise AssertionError("unreachable")
 
     async def post(self, obj: Dict) -> Dict:
         return await asyncio.get_running_loop().run_in_executor(None, self._post, obj)

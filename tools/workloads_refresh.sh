@@ -1,8 +1,8 @@
 #!/bin/bash
-# Re-run every bench.py workload of profiles/r01_bench_workloads.jsonl on the GPU box, one line each,
+# Re-run every bench.py workload of profiles/rNN_bench_workloads.jsonl on the GPU box, one line each,
 # into gpurun_out/workloads_TAG.jsonl.  Each step has its own time limit; the chain stops at a failure.
 set -o pipefail
-TAG=${1:-r01}
+TAG=${1:-r02}
 OUT=gpurun_out/workloads_$TAG.jsonl
 mkdir -p gpurun_out && : > $OUT
 B="python3 bench.py --no-cpu-baseline"
