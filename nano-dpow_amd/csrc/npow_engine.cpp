@@ -69,7 +69,7 @@ std::atomic<uint32_t> g_blocks_per_cu{8};
 std::atomic<uint32_t> g_budget_us{20000};  // pool launches end on time, not on their slowest wave
 // Pool launches: 4 workgroups (16 waves) per CU.  Four waves per SIMD already saturate VALU
 // issue under the time budget (27.05 Gnonce/s at 4, 5 and 6 per CU), and the pool kernel's
-// ~100 SGPRs admit only 6 per CU (tools/wave_probe.cpp: with 8 requested, 2 per CU start
+// ~100 SGPRs admit only 6 per CU (tools/experiments/wave_probe.cpp: with 8 requested, 2 per CU start
 // only when the first 6 finish), so 4 leaves room for compiler changes.
 std::atomic<uint32_t> g_pool_blocks_per_cu{4};
 

@@ -328,7 +328,7 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
   // Time budget.  VALU issue on a SIMD goes to its OLDEST wave first (MI355X_MICROARCH.md:
   // priority, then age), so the 8 waves of a SIMD do not progress together: the oldest runs
   // at single-wave speed and finishes first, the youngest barely runs until the others are
-  // done (tools/wave_probe.cpp: wave finish times 1.0 - 5.6 ms in a 5.6-ms launch).  A launch
+  // done (tools/experiments/wave_probe.cpp: wave finish times 1.0 - 5.6 ms in a 5.6-ms launch).  A launch
   // of a fixed iteration count therefore ends in a tail where one or two waves per SIMD are
   // left.  Unbounded entries need no fixed partition, so every wave instead stops at the same
   // wall-clock point, its own start (read first thing, before any VALU instruction the age
@@ -427,7 +427,7 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
     pool_load(&tab->e[e], c, false, w, W, n, e, iters);
   }
 #ifdef NPOW_WAVE_PROBE
-  // diagnostic build (tools/wave_probe.cpp): per-wave start / end realtime, iterations, HW ids
+  // diagnostic build (tools/experiments/wave_probe.cpp): per-wave start / end realtime, iterations, HW ids
   if (lane == 0) {
     npow_wave_probe[w * 4 + 0] = t_start;
     npow_wave_probe[w * 4 + 1] = __builtin_amdgcn_s_memrealtime();

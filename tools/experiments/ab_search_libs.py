@@ -1,7 +1,7 @@
 """Interleaved A/B of two libnanopow builds in ONE process on the bench workload (first-win
 searches at fffffff800000000) and a no-hit sweep.  Each build is loaded through its own copy
 of the ctypes shim (A_SHIM / B_SHIM: paths of _lib.py files matching each build).
-A=path.so B=path.so A_SHIM=... B_SHIM=... ROUNDS=3 N_SEARCH=60 python3 tools/ab_search_libs.py"""
+A=path.so B=path.so A_SHIM=... B_SHIM=... ROUNDS=3 N_SEARCH=60 python3 tools/experiments/ab_search_libs.py"""
 import hashlib, importlib.util, json, os, statistics, sys, time
 
 M64 = (1 << 64) - 1

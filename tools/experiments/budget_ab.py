@@ -1,9 +1,9 @@
 """Launch time budget A/B through the engine: an unbounded never-hit job run for a fixed time
 (then cancelled) and the bench's first-win searches, at several budgets (0 = iteration count).
-Usage: python3 tools/budget_ab.py 0 5000 [iters]"""
+Usage: python3 tools/experiments/budget_ab.py 0 5000 [iters]"""
 import json, os, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "nano-dpow_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "nano-dpow_amd"))
 import bench
 from nanopow import _lib
 e = _lib.Engine()

@@ -1,8 +1,8 @@
 """No-hit bounded searches (threshold 2^64-1, exact 2^34 nonces) through the engine at several
 iterations per launch: kernel and wall Gnonce/s, to separate steady-state rate from per-search
-effects.  Usage: python3 tools/iters_nohit.py 256 1024 4096"""
+effects.  Usage: python3 tools/experiments/iters_nohit.py 256 1024 4096"""
 import json, os, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "nano-dpow_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "nano-dpow_amd"))
 from nanopow import _lib
 e = _lib.Engine()
 M64 = (1 << 64) - 1

@@ -1,8 +1,8 @@
 """Same 100 bench searches at two iterations-per-launch settings: winners, nonces hashed and wall
-time per search, to see where a longer launch gains.  Usage: python3 tools/iters_search_ab.py 256 4096"""
+time per search, to see where a longer launch gains.  Usage: python3 tools/experiments/iters_search_ab.py 256 4096"""
 import json, os, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), ".."))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "nano-dpow_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", ".."))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "nano-dpow_amd"))
 import bench
 from nanopow import _lib
 e = _lib.Engine()

@@ -1,7 +1,7 @@
 """Interleaved A/B of kernel throughput: search vs sweep mode, iterations per launch, blocks per CU.
 Same work in every arm (threshold 2^64-1: no hits, so no early exit); kernel time from HIP events."""
 import json, os, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'nano-dpow_amd'))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..', 'nano-dpow_amd'))
 from nanopow import _lib
 e = _lib.Engine(os.environ.get("NANOPOW_LIB", _lib.LIB_PATH))
 M64 = (1 << 64) - 1

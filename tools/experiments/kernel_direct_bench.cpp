@@ -3,7 +3,7 @@
 //   task  = npow_task_kernel<kSweep> (kernel-argument uniforms, one root; no hits)
 //   pool1 = npow_pool_kernel<false> with one unbounded entry
 //   pool8 = npow_pool_kernel<false> with eight unbounded entries
-// Build: hipcc -O3 --offload-arch=gfx950 -Inano-dpow_amd/csrc -Iinclude -x hip tools/kernel_direct_bench.cpp
+// Build: hipcc -O3 --offload-arch=gfx950 -Inano-dpow_amd/csrc -Iinclude -x hip tools/experiments/kernel_direct_bench.cpp
 //        -x none nano-dpow_amd/csrc/npow_kernel.o -o build/kernel_direct_bench
 // Run:   ./build/kernel_direct_bench [reps] [iters] [poll_mask] [gap_us] [blocks_per_cu]
 #include <hip/hip_runtime.h>

@@ -1,7 +1,7 @@
 """Interleaved A/B of several libnanopow.so builds in ONE process (guide §5.4 rule 24).
-LIBS=a.so,b.so ROUNDS=3 python3 tools/lib_ab.py -> median kernel Gnonce/s per build (sweep, no hits)."""
+LIBS=a.so,b.so ROUNDS=3 python3 tools/experiments/lib_ab.py -> median kernel Gnonce/s per build (sweep, no hits)."""
 import ctypes, json, os, statistics, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'nano-dpow_amd'))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..', 'nano-dpow_amd'))
 from nanopow import _lib
 libs = os.environ["LIBS"].split(",")
 engines = []

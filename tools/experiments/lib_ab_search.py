@@ -1,7 +1,7 @@
 """Interleaved A/B of libnanopow builds in ONE process on the bench workload (first-win searches at
 fffffff800000000) and on a no-hit sweep.  LIBS=a.so,b.so ROUNDS=3 N_SEARCH=60."""
 import hashlib, json, os, statistics, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'nano-dpow_amd'))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..', 'nano-dpow_amd'))
 from nanopow import _lib
 libs = os.environ["LIBS"].split(",")
 engines = []

@@ -1,6 +1,6 @@
 """Sweep (no hits) kernel rate at several host-abort poll intervals, one process, plus cancel latency."""
 import json, os, sys, threading, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'nano-dpow_amd'))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..', 'nano-dpow_amd'))
 from nanopow import _lib
 e = _lib.Engine(os.environ.get("NANOPOW_LIB", _lib.LIB_PATH))
 M64 = (1 << 64) - 1

@@ -1,7 +1,7 @@
 """Sweep kernel (npow_task_kernel<kSweep>) throughput at several workgroups-per-CU settings:
-exact 2^34-nonce no-hit sweeps.  Usage: python3 tools/sweep_bpc.py 6,7,8"""
+exact 2^34-nonce no-hit sweeps.  Usage: python3 tools/experiments/sweep_bpc.py 6,7,8"""
 import json, os, sys, time
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "nano-dpow_amd"))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "nano-dpow_amd"))
 from nanopow import _lib
 e = _lib.Engine()
 M64 = (1 << 64) - 1

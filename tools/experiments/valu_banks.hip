@@ -2,7 +2,7 @@
 // gfx950?  Streams of 16 independent instructions per iteration with explicit registers:
 // each variant fixes the (dst, src0, src1) register numbers mod 4 (the bank, if banks are
 // index mod 4).  8 waves/SIMD (256 CUs x 8 blocks x 256 lanes), in-kernel clock.
-// Build: hipcc --offload-arch=gfx950 -O3 -o build/valu_banks tools/valu_banks.hip
+// Build: hipcc --offload-arch=gfx950 -O3 -o build/valu_banks tools/experiments/valu_banks.hip
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

@@ -1,7 +1,7 @@
 """A/B helper: parity + sweep throughput of one libnanopow.so variant (NANOPOW_LIB)."""
 import os, sys, time, random, json
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'nano-dpow_amd'))
-sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'oracle'))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..', 'nano-dpow_amd'))
+sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', '..', 'oracle'))
 import nanopow, oracle
 from nanopow import _lib
 e = _lib.Engine(os.environ.get("NANOPOW_LIB", _lib.LIB_PATH))

@@ -1,7 +1,7 @@
 // wave_probe.cpp -- diagnostic: per-wave timing of one npow_pool_kernel launch (kernel built with
 // -DNPOW_WAVE_PROBE).  Prints the spread of wave start / end times and of iteration rates per XCD
 // and per SIMD, to see whether a full launch ends with a slow tail.
-// Build: hipcc -O3 --offload-arch=gfx950 -Inano-dpow_amd/csrc -Iinclude -x hip tools/wave_probe.cpp
+// Build: hipcc -O3 --offload-arch=gfx950 -Inano-dpow_amd/csrc -Iinclude -x hip tools/experiments/wave_probe.cpp
 //        -o build/wave_probe
 #include <hip/hip_runtime.h>
 

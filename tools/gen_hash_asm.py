@@ -284,7 +284,7 @@ def next_carry() -> str:
 ROT_MAD = lambda n, h: False  # which rotr16/24 halves use v_lshrrev_b32 + v_mad_u32_u24 (--rotmad)
 ROTL1_CC = False  # rotr63 = x + x + carry as v_add_co_u32 + 2x v_addc_co_u32
 ROTL1_VIA_ADD = True  # rotr63 = (x << 1) + (x >> 63): v_lshrrev_b32 + v_lshl_add_u64 with a zero partner
-# Measured on MI355X (tools/valu_patterns.py): in a stream that mixes in 64-bit / 3-operand VALU
+# Measured on MI355X (tools/experiments/valu_patterns.py): in a stream that mixes in 64-bit / 3-operand VALU
 # ops, VOP2-encoded v_xor_b32 issues at ~4.1 SIMD cycles but its VOP3 (_e64) encoding at ~2.6.
 VOP3_SIMPLE = True
 # rotr32 as two in-place xors + two v_mov_b32 into the fresh pair (movs issue nearly free)
@@ -1023,7 +1023,7 @@ def c_expr_program(frontier: List[Node]) -> List[str]:
     return out
 
 
-# Code placement (measured on MI355X, tools/hash_clock.hip): the same all-8-byte instruction stream
+# Code placement (measured on MI355X, tools/experiments/hash_clock.hip): the same all-8-byte instruction stream
 # runs 11 % faster when its instructions sit at byte offsets = 4 (mod 8) than at 0 (mod 8).  The asm
 # block therefore opens with ".p2align 3" + one 4-byte s_nop, and every instruction inside it is
 # 8 bytes long (VOP3 encodings; VOP2 only with a 32-bit literal), so the parity holds throughout.
