@@ -124,13 +124,19 @@ def test_sweep_capacity_error(gpu_engine):
 @pytest.mark.parametrize("thr", [LOW, RECEIVE, SEND])
 def test_search_results_revalidate(gpu_engine, thr):
     rng = random.Random(thr)
-    n = 40 if thr != SEND else 12
+    n = 64
+    done = 0
     for _ in range(n):
         root = bytes(rng.getrandbits(8) for _ in range(32))
         r = gpu_engine.search(root, thr, start=rng.getrandbits(64))
         assert r.status == _lib.NPOW_OK
         assert oracle.work_value_hashlib(root, r.nonce) == r.value >= thr
         assert r.nonces_done > 0
+        done += r.nonces_done
+    # nonces per search: a geometric number with mean 2^64 / (2^64 - thr) plus the rest of the
+    # launch after the win; over 64 searches the mean stays within a factor 3 of the expectation
+    expect = (1 << 64) / ((1 << 64) - thr)
+    assert expect / 3 < done / n < 3 * expect + (1 << 22), (done / n, expect)
 
 
 def test_search_is_first_in_small_ranges(gpu_engine):

@@ -57,8 +57,21 @@ def test_send_difficulty_generate_and_validate(gpu_server):
 
 
 def test_benchmark_on_gpu(gpu_server):
-    r = post(gpu_server.address, {"action": "benchmark", "count": 10})
-    assert r["count"] == "10" and int(r["duration"]) > 0
+    """`benchmark` (nano-work-server.exe @1679992..1680344): count searches of random roots at the
+    base difficulty, timed end to end; fields and arithmetic as the reference reports them."""
+    t = time.perf_counter()
+    r = post(gpu_server.address, {"action": "benchmark", "count": 32})
+    wall_ms = (time.perf_counter() - t) * 1e3
+    assert set(r) == {"count", "difficulty", "multiplier", "duration", "average", "hint"}
+    assert r["count"] == "32" and r["difficulty"] == "fffffff800000000" and float(r["multiplier"]) == 1.0
+    assert r["hint"] == "Times in milliseconds"
+    d, a = int(r["duration"]), int(r["average"])
+    assert 0 < d <= wall_ms + 1 and abs(a - d / 32) <= 1
+    # 32 searches at 2^29 expected nonces each on one MI355X (~27 Gnonce/s): ~20 ms apiece
+    assert 2 <= a <= 200, r
+    # at receive difficulty (2^23 expected nonces) every search is sub-millisecond on average
+    r = post(gpu_server.address, {"action": "benchmark", "count": 50, "difficulty": "fffffe0000000000"})
+    assert r["difficulty"] == "fffffe0000000000" and float(r["multiplier"]) == 1 / 64 and int(r["average"]) <= 5
 
 
 def test_dpow_messages_to_results_on_gpu(gpu_engine):
