@@ -477,6 +477,10 @@ void Worker::check_slots() {
     if (sl.state != SlotState::kActive) continue;
     Job& j = *sl.job;
     if (d_.dead) {  // dropped device: stop every job's waves; retire() re-strides them
+      if (j.max_per_dev) {  // the killed launches leave their ranges unfinished: hand them back
+        std::lock_guard<std::mutex> g(g_pool.mu);
+        push_back_locked(sl, 0);
+      }
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);
       sl.state = SlotState::kDraining;
     } else if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {

@@ -12,7 +12,12 @@ Mix (per client thread, chosen at random each round):
   * small exact sweeps checked against the C oracle;
   * max_active and launch-budget changes from a separate thread (yields, queueing).
 
-Usage (GPU box): python3 tools/pool_soak.py [--seconds 180] [--clients 24]
+With --faults (run with NANOPOW_VIRTUAL_DEVICES and NANOPOW_FAULT_INVALID, npow_pool.cpp): bounded
+ranges run over every device too, and must end EXHAUSTED having hashed at least n nonces per device
+alive when they were submitted, less one device (a device dropped mid-job hands what it had not
+finished to the others, which may hash part of it again); searches must still all succeed.
+
+Usage (GPU box): python3 tools/pool_soak.py [--seconds 180] [--clients 24] [--faults]
 """
 import argparse
 import json
@@ -38,6 +43,7 @@ def main():
     ap.add_argument("--seconds", type=float, default=180.0)
     ap.add_argument("--clients", type=int, default=24)
     ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--faults", action="store_true", help="a fault hook is set: bounded ranges over every device")
     args = ap.parse_args()
     eng = _lib.Engine()
     stop = time.time() + args.seconds
@@ -86,10 +92,17 @@ def main():
                         fail(f"cancel {root.hex()}: {r}")
                 elif kind < 0.85:
                     n = rng.choice([1, 63, 64, 65, 1000, 4097, 1 << 16, (1 << 20) + 3, 1 << 24])
-                    r = eng.submit(root, M64, start=rng.getrandbits(64), device_mask=1,
-                                   max_nonces_per_device=n).wait(120)
-                    if r is None or r.status != _lib.NPOW_EXHAUSTED or r.nonces_done != n:
-                        fail(f"bounded {n}: {r}")
+                    if args.faults:
+                        alive = sum(1 for d in range(eng.n_devices) if not eng.stats(d).dead)
+                        r = eng.submit(root, M64, start=rng.getrandbits(64), device_mask=0,
+                                       max_nonces_per_device=n).wait(120)
+                        if r is None or r.status != _lib.NPOW_EXHAUSTED or r.nonces_done < n * (alive - 1):
+                            fail(f"bounded {n} over {alive} devices: {r}")
+                    else:
+                        r = eng.submit(root, M64, start=rng.getrandbits(64), device_mask=1,
+                                       max_nonces_per_device=n).wait(120)
+                        if r is None or r.status != _lib.NPOW_EXHAUSTED or r.nonces_done != n:
+                            fail(f"bounded {n}: {r}")
                     bump("bounded")
                 else:
                     start, cnt = rng.getrandbits(64), rng.choice([1000, 65536, 1 << 20])
@@ -131,7 +144,8 @@ def main():
     st = eng.stats(0)
     out = {"seconds": round(time.time() - t0, 1), "clients": args.clients, "counts": counts,
            "errors": errors[:5], "pool_status_end": list(eng.pool_status()), "device0_nonces": st.nonces,
-           "device0_invalid": st.invalid if hasattr(st, "invalid") else None}
+           "invalid_work": [eng.stats(d).invalid_work for d in range(eng.n_devices)],
+           "dead": [eng.stats(d).dead for d in range(eng.n_devices)]}
     print(json.dumps(out), flush=True)
     return 1 if errors or tuple(eng.pool_status()) != (0, 0) else 0
 
