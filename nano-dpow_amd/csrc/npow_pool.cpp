@@ -65,11 +65,11 @@ constexpr double kPrelaunchUs = 2000.0;  // queue the next launch when the runni
 constexpr double kFreshSpinUs = 400.0;   // poll without sleeping this long after a launch starts (quick wins)
 constexpr int kInvalidStreakMax = 3;     // consecutive invalid results that drop a device (@1669144)
 // Between steps a worker with a launch in flight sleeps this long (wakes early on new jobs):
-// a win is seen within it, and the thread costs a few % of a core instead of spinning.
+// a win is seen within it, and the thread costs ~6 % of a core instead of spinning (nap()).
 // NANOPOW_POLL_US overrides (0 = spin).
 const double g_poll_us = [] {
   const char* e = getenv("NANOPOW_POLL_US");
-  return e ? atof(e) : 100.0;
+  return e ? atof(e) : 50.0;
 }();
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
 const bool g_trace_lat = getenv("NANOPOW_TRACE_LATENCY") != nullptr;
@@ -760,8 +760,9 @@ void Worker::run() {
 // job is decided or cancelled, new jobs arrive (they notify cv_work) or the next launch must be
 // queued: poll without sleeping only during the first kFreshSpinUs of a launch (wins at receive
 // difficulty come that early) and near the next launch's queueing point; otherwise sleep up to
-// g_poll_us on cv_work.  A win is then seen within ~g_poll_us (~0.25 % of a send-difficulty
-// search at 100 us) and the thread uses a few % of a core instead of all of it.
+// g_poll_us on cv_work.  A win is then seen within ~g_poll_us and the thread uses ~6 % of a core
+// instead of all of it (50 us: 27.13 Gnonce/s on the serial bench vs 27.07 spinning, 26.98 at
+// 200 us; profiles/r02_ab_worker_nap.txt).
 void Worker::nap() {
   if (g_poll_us <= 0 || q_.empty() || d_.dead || d_.tasks_waiting.load() > 0) {
     cpu_relax();
