@@ -35,6 +35,13 @@ PATTERNS = {
     "addco4|addc4 sgpr-rot": ["addco4a", "addc4a"], "addco6 sgpr-rot": ["addco8"],
     "xor xor|addco4 addc4 sgpr-rot": ["xor", "xor", "addco4b", "addc4b"],
     "xor|addco6 sgpr-rot alt": ["xor", "addco8"],
+    # free fillers beside half-rate ops, and fillers at half -> full transitions (round 2)
+    "mov|add64 alt": ["mov", "add64"], "mov e64|align alt": ["mov3", "align"], "not|align alt": ["not", "align"],
+    "mov64|align alt": ["mov64", "align"], "movsdwa|align alt": ["movsdwa", "align"],
+    "xorsdwa|align alt": ["xorsdwa", "align"], "movdpp|align alt": ["movdpp", "align"],
+    "align mov xor": ["align", "mov", "xor"], "align mov e64 xor": ["align", "mov3", "xor"],
+    "add64 mov xor": ["add64", "mov", "xor"], "add64 xor": ["add64", "xor"],
+    "align mov mov xor": ["align", "mov", "mov", "xor"], "xor align mov": ["xor", "align", "mov"],
     "lshl": ["lshl"], "or": ["or"], "lshr64": ["lshr64"], "add3": ["add3"], "addu": ["addu"],
     "xor|alignbyte alt": ["xor", "alignbyte"], "xor|lshlor alt": ["xor", "lshlor"],
     "xor xor|addco addc": ["xor", "xor", "addco", "addc"],
@@ -128,6 +135,8 @@ def emit2(kind, i):
     if kind == "addco8":  # six rotating pairs, carry-out only
         k = 20 + 2 * (i % 6)
         return f"v_add_co_u32_e64 v{d}, s[{k}:{k + 1}], v{s0}, v{s1}"
+    if kind == "mov3":
+        return f"v_mov_b32_e64 v{d}, v{s0}"
     if kind == "lshlor":
         return f"v_lshl_or_b32 v{d}, v{s0}, 8, v{s1}"
     if kind == "lshl":
