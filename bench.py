@@ -327,11 +327,14 @@ def node_time_to_work(eng, dev: int, rank: int, world: int, dist, m: int, thr: i
     dist.all_gather_object(gathered, recs)
     if rank != 0:
         return None
-    ttw, failed, nonces = [], 0, 0
+    ttw, failed, nonces, busy = [], 0, 0, 0.0
     cancelled = sum(1 for g in gathered for rec in g if rec[1] == 1)
     for i in range(m):
         wins = [g[i][0] for g in gathered if g[i][1] == 0]
         nonces += sum(g[i][2] for g in gathered)
+        # the root occupies the node until its last rank returns (the winner, or a rank that saw
+        # the winner's cancel word): the node's search time for that root
+        busy += max((g[i][0] for g in gathered if g[i][0] is not None), default=0.0)
         if wins:
             ttw.append(min(wins))
         else:
@@ -343,6 +346,9 @@ def node_time_to_work(eng, dev: int, rank: int, world: int, dist, m: int, thr: i
             "rank_searches_cancelled": cancelled,
             "shared_cancel": words.path is not None,
             "nonces_per_search": round(nonces / m),
+            "node_gnps": round(nonces / busy / 1e9, 4) if busy > 0 else None,
+            "node_gnps_note": "nonces hashed by all ranks / sum over roots of the time until the root's last rank "
+                              "returned (per-root barriers excluded): the node's rate on one root at a time",
             "note": f"one root at a time searched by all {world} ranks on disjoint strides (rank r from "
                     "start + r*2^64/N), the first win cancelling the others through a shared-memory word; "
                     "winner's search time at the C ABI; after the timed region, not part of value"}
@@ -1029,7 +1035,7 @@ def main() -> int:
     ap.add_argument("--cpu-requests", type=int, default=4, help="receive: requests timed on the CPU reference")
     ap.add_argument("--via", choices=["abi", "http"], default="abi",
                     help="burst: submit through the C ABI work pool or POST to the HTTP work server")
-    ap.add_argument("--node-searches", type=int, default=100,
+    ap.add_argument("--node-searches", type=int, default=300,
                     help="search, N>1: roots searched by all ranks at once after the timed steps (node time-to-work)")
     ap.add_argument("--http-requests", type=int, default=100,
                     help="search, N=1: work_generate requests timed at the JSON boundary after the timed steps")

@@ -138,6 +138,7 @@ def test_node_time_to_work_cross_rank_first_win():
     out = got[0][0]
     assert got[1][0] is None and out["n"] == 12 and out["failed"] == 0 and out["shared_cancel"]
     assert out["p50"] > 0 and out["p99"] >= out["p50"]
+    assert out["node_gnps"] > 0 and out["nonces_per_search"] > 0
     assert out["rank_searches_cancelled"] >= 6  # the slow rank is cancelled by the winner's word
     # disjoint strides: rank 1 starts half the nonce space away from rank 0, root by root
     for s0, s1 in zip(got[0][1], got[1][1]):
