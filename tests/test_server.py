@@ -300,3 +300,77 @@ def test_reference_workhandler_against_this_server():
                                                               else "precache")
         v = oracle.work_value_hashlib(bytes.fromhex(c["hash"]), int(c["work"], 16))
         assert v >= thr and int(rep["difficulty"], 16) == v
+
+
+def _raw(addr, data: bytes, timeout=10) -> bytes:
+    """Send raw bytes on one connection and read until the server closes it."""
+    import socket
+    host, port = addr.rsplit(":", 1)
+    s = socket.create_connection((host, int(port)), timeout=timeout)
+    try:
+        s.sendall(data)
+        chunks = []
+        while True:
+            b = s.recv(65536)
+            if not b:
+                break
+            chunks.append(b)
+        return b"".join(chunks)
+    finally:
+        s.close()
+
+
+def _replies(raw: bytes):
+    """Split a byte stream of HTTP/1.1 responses into (status, headers, json body)."""
+    out = []
+    while raw:
+        head, _, rest = raw.partition(b"\r\n\r\n")
+        lines = head.split(b"\r\n")
+        status = int(lines[0].split()[1])
+        hdrs = {k.strip().lower(): v.strip() for k, _, v in (ln.partition(b":") for ln in lines[1:])}
+        n = int(hdrs[b"content-length"])
+        out.append((status, hdrs, json.loads(rest[:n]) if n else None))
+        raw = rest[n:]
+    return out
+
+
+def test_http_keepalive_pipelining_and_close(server):
+    """The connection handler (nanopow/server.py _Connection): several requests on one keep-alive
+    connection, pipelined, answered in order; `Connection: close` ends it after its reply."""
+    srv, _ = server
+    body = json.dumps({"action": "status"}).encode()
+    one = b"POST / HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body)
+    last = b"POST / HTTP/1.1\r\nHost: x\r\nConnection: close\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body)
+    got = _replies(_raw(srv.address, one + one + last))
+    assert [g[0] for g in got] == [200, 200, 200]
+    assert all(g[2] == {"generating": "0", "queue_size": "0"} for g in got)
+    assert got[-1][1].get(b"connection") == b"close" and all(g[1][b"content-type"] == b"application/json" for g in got)
+
+
+def test_http_chunked_body_expect_continue_and_http10(server):
+    srv, _ = server
+    body = json.dumps({"action": "invalid"}).encode()
+    chunked = (b"POST / HTTP/1.1\r\nTransfer-Encoding: chunked\r\nConnection: close\r\n\r\n"
+               + b"%x\r\n%s\r\n" % (5, body[:5]) + b"%x\r\n%s\r\n" % (len(body) - 5, body[5:]) + b"0\r\n\r\n")
+    (st, _, rep), = _replies(_raw(srv.address, chunked))
+    assert st == 200 and rep["error"] == "Unknown command"
+    cont = _raw(srv.address, b"POST / HTTP/1.1\r\nExpect: 100-continue\r\nConnection: close\r\nContent-Length: %d\r\n\r\n%s"
+                % (len(body), body))
+    assert cont.startswith(b"HTTP/1.1 100 Continue\r\n\r\n")
+    (st, _, rep), = _replies(cont[len(b"HTTP/1.1 100 Continue\r\n\r\n"):])
+    assert st == 200 and rep["error"] == "Unknown command"
+    # HTTP/1.0 without keep-alive: one reply, then the server closes
+    (st, hdrs, rep), = _replies(_raw(srv.address, b"POST / HTTP/1.0\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body)))
+    assert st == 200 and hdrs.get(b"connection") == b"close"
+
+
+def test_http_malformed_requests_are_answered_and_closed(server):
+    srv, _ = server
+    (st, _, rep), = _replies(_raw(srv.address, b"GARBAGE\r\n\r\n"))
+    assert st == 400
+    (st, _, rep), = _replies(_raw(srv.address, b"POST / HTTP/1.1\r\nContent-Length: 99999999\r\n\r\n"))
+    assert st == 413
+    (st, _, rep), = _replies(_raw(srv.address, b"POST / HTTP/1.1\r\nContent-Length: x\r\n\r\n"))
+    assert st == 400
+    (st, _, rep), = _replies(_raw(srv.address, b"GET / HTTP/1.1\r\nConnection: close\r\n\r\n"))
+    assert st == 405 and rep == {"error": "Can only POST requests"}
