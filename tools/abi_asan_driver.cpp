@@ -41,6 +41,13 @@ static void make_root(uint64_t seed, uint8_t root[32]) {
   }
 }
 
+// Devices of the searches, tickets and bounded ranges: DRIVER_MASK (default 1 = device 0; 0 = every
+// device, with NANOPOW_VIRTUAL_DEVICES / NANOPOW_FAULT_* to drive the device-drop path).
+static const uint64_t g_mask = [] {
+  const char* e = std::getenv("DRIVER_MASK");
+  return e ? std::strtoull(e, nullptr, 0) : 1ull;
+}();
+
 // first-win searches at an easy threshold, re-validated on the CPU
 static void searches(int tid, int n) {
   for (int i = 0; i < n; i++) {
@@ -48,7 +55,7 @@ static void searches(int tid, int n) {
     make_root(1000 * tid + i, root);
     const uint64_t thr = 0xfffff00000000000ull;
     uint64_t nonce = 0, value = 0, done = 0;
-    int rc = npow_search(root, thr, uint64_t(i) << 40, 1, 0, nullptr, &nonce, &value, &done);
+    int rc = npow_search(root, thr, uint64_t(i) << 40, g_mask, 0, nullptr, &nonce, &value, &done);
     CHECK(rc == NPOW_OK, "search rc %d", rc);
     CHECK(value == npow_work_value(root, nonce) && value >= thr, "search value");
     g_won++;
@@ -63,7 +70,7 @@ static void tickets(int tid, int n) {
     volatile uint32_t cancel = 0;
     uint64_t ticket = 0;
     const uint64_t thr = (i % 3 == 0) ? 0xffffffffffff0000ull : 0xfffffe0000000000ull;
-    int rc = npow_submit(root, thr, 0, 1, 0, &cancel, &ticket);
+    int rc = npow_submit(root, thr, 0, g_mask, 0, &cancel, &ticket);
     CHECK(rc == NPOW_OK, "submit rc %d", rc);
     uint64_t nonce = 0, value = 0, done = 0;
     rc = npow_wait(ticket, 2000, &nonce, &value, &done);
@@ -100,7 +107,7 @@ static void sweeps(int tid, int n) {
       CHECK(out[k] == ref[k], "sweep hit %llu", (unsigned long long)k);
 
     uint64_t nonce = 0, value = 0, done = 0;
-    rc = npow_search(root, ~uint64_t(0), start, 1, 4096 + i, nullptr, &nonce, &value, &done);
+    rc = npow_search(root, ~uint64_t(0), start, g_mask, 4096 + i, nullptr, &nonce, &value, &done);
     CHECK(rc == NPOW_EXHAUSTED || rc == NPOW_OK, "bounded rc %d", rc);
     if (rc == NPOW_EXHAUSTED) g_exhausted++;
   }
