@@ -196,6 +196,11 @@ void free_device(Device& d) {
 int init_device(Device& d, int n_physical) {
   d.hip_id = d.id % n_physical;
   HIPTRY(hipSetDevice(d.hip_id));
+  if (const char* f = getenv("NANOPOW_FAULT_INIT"))  // test hook: this logical device fails to open
+    if (atoi(f) == d.id) {
+      HIPTRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));  // something to clean up
+      return fail(NPOW_ERR_HIP, "injected init failure (NANOPOW_FAULT_INIT)");
+    }
   hipDeviceProp_t p;
   HIPTRY(hipGetDeviceProperties(&p, d.hip_id));
   d.cus = p.multiProcessorCount;

@@ -28,7 +28,7 @@
 // covered exactly once more).  A job fails only when no device is left to search it.
 // Test hooks (environment, read once): NANOPOW_FAULT_INVALID=d[,d...] makes the host read a
 // corrupted value for every win of those logical devices; NANOPOW_FAULT_HIP=d:n makes device
-// d's launches fail after its n-th.
+// d's launches fail after its n-th.  (npow_engine.cpp: NANOPOW_FAULT_INIT=d fails npow_init on d.)
 #include <hip/hip_runtime.h>
 #include <sys/prctl.h>
 #include <time.h>

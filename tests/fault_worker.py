@@ -16,6 +16,8 @@ work 3 consecutive times" and re-validates every GPU result on the CPU
   allbad    NANOPOW_FAULT_INVALID=0,1, 2 devices: both devices only return invalid work; the
             search fails with NPOW_ERR_INVALID_WORK once the second one is dropped, and a new
             search has no device left (NPOW_ERR_NO_DEVICE).
+  init      NANOPOW_FAULT_INIT=2, 4 devices: npow_init fails while opening device 2; a retry
+            (hook removed) opens all 4 cleanly.
 
 Prints one JSON line; exits non-zero on any mismatch."""
 import json
@@ -134,8 +136,36 @@ def scenario_allbad(eng, G):
     return {}
 
 
+def scenario_init():
+    """npow_init failing on device 2 of 4 leaves nothing behind: the retry opens 4 devices, ids
+    0..3 in order, each serving its own searches (a partial init used to leave
+    duplicate devices and leaked streams)."""
+    try:
+        _lib.Engine()
+        raise AssertionError("npow_init ignored NANOPOW_FAULT_INIT")
+    except _lib.NanoPowError as e:
+        assert e.code == _lib.NPOW_ERR_HIP and "NANOPOW_FAULT_INIT" in e.message, e
+    del os.environ["NANOPOW_FAULT_INIT"]
+    eng = _lib.Engine()
+    G = eng.n_devices
+    assert G == 4, G
+    rng = random.Random(9)
+    for d in range(G):
+        eng.reset_stats(d)
+        rt = bytes(rng.getrandbits(8) for _ in range(32))
+        r = eng.search(rt, RECEIVE, device_mask=1 << d)
+        assert valid(rt, r, RECEIVE) and eng.stats(d).launches > 0
+        assert all(eng.stats(k).launches == 0 for k in range(d + 1, G))
+    return {"devices_after_retry": G}
+
+
 def main():
     which = sys.argv[1]
+    if which == "init":
+        out = scenario_init()
+        out.update({"scenario": which, "devices": 4, "ok": True})
+        print(json.dumps(out), flush=True)
+        return
     eng = _lib.Engine()
     G = eng.n_devices
     assert G == int(os.environ["NANOPOW_VIRTUAL_DEVICES"]), G

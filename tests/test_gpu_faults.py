@@ -19,6 +19,7 @@ SCENARIOS = {
     "hip": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_HIP": "2:3"},
     "exhaust": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_HIP": "2:3"},
     "allbad": {"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_FAULT_INVALID": "0,1"},
+    "init": {"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_FAULT_INIT": "2"},
 }
 
 
