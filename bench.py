@@ -83,13 +83,20 @@ sys.path.insert(0, os.path.join(HERE, "nano-dpow_amd"))
 SEND = 0xfffffff800000000
 OPS_PER_NONCE = 2232                # int32 VALU ops of one 12-round compression
 PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # MI355X: 256 CU x (4 SIMD x 32 lanes) x 2.4 GHz = 78.6 Tops/s
-# The instruction stream's own issue bound (informational, next to the roofline): the generated hash
-# costs 5,725 SIMD cycles per wave (64 nonces) with every SIMD saturated and no launch tail
-# (tools/valu_mix2.py "real hash stream", 20-ms budget, two runs: profiles/r01_valu_mix2_final_stream.jsonl):
-# 1,671 instructions, half of them half rate, at 3.426 cycles each.
-STREAM_CYCLES_PER_HASH = 5725
+# The instruction stream's own issue bound (informational, next to the roofline), per search kernel:
+#  * lockstep (default): the barrier-interval stream, 1,675 VALU instructions, 5,251 SIMD cycles per
+#    wave (64 nonces) with one 1,024-lane workgroup per CU and no launch tail
+#    (tools/experiments/stream_lockstep.py, profiles/r02_stream_lockstep.jsonl), 3.135 cycles each;
+#  * seq (NANOPOW_POOL_KERNEL=seq): 1,671 instructions at 5,725 cycles, time-budgeted, every SIMD
+#    saturated (tools/valu_mix2.py "real hash stream": profiles/r01_valu_mix2_final_stream.jsonl).
+POOL_KERNEL = "seq" if os.environ.get("NANOPOW_POOL_KERNEL") == "seq" else "lockstep"
+STREAM = {"lockstep": {"cycles": 5251, "valu": 1675, "kernel": "npow_pool_kernel_ls_arg<false>",
+                       "src": "tools/experiments/stream_lockstep.py, profiles/r02_stream_lockstep.jsonl"},
+          "seq": {"cycles": 5725, "valu": 1671, "kernel": "npow_pool_kernel_arg<false>",
+                  "src": "tools/valu_mix2.py, profiles/r01_valu_mix2_final_stream.jsonl"}}[POOL_KERNEL]
+STREAM_CYCLES_PER_HASH = STREAM["cycles"]
 STREAM_CLOCK_GHZ = 2.39   # in-kernel s_memtime / s_memrealtime under this load
-STREAM_BOUND_GNPS = 1024 * 64 * STREAM_CLOCK_GHZ / STREAM_CYCLES_PER_HASH  # 1,024 SIMDs: 27.35
+STREAM_BOUND_GNPS = 1024 * 64 * STREAM_CLOCK_GHZ / STREAM_CYCLES_PER_HASH  # 1,024 SIMDs
 METRIC = "Gnonce/s blake2b-64 per GPU & 8-GPU node; p50 time-to-work at fffffff8"
 
 
@@ -510,7 +517,7 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
         "gnps_per_gpu": round(gnps / world, 4),
         "roofline": {
             "bound": "valu",
-            "kernel": "npow_pool_kernel<false>",
+            "kernel": STREAM["kernel"],
             "achieved": round(achieved, 3),
             "peak": round(PEAK_TOPS, 3),
             "unit": "Tops/s (int32 VALU)",
@@ -526,9 +533,11 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
                 "gnps": round(STREAM_BOUND_GNPS, 3),
                 "kernel_frac": (round(kern_nonces / (kern_ms * 1e-3) / 1e9 / STREAM_BOUND_GNPS, 4)
                                 if kern_ms > 0 else None),
-                "what": "measured issue bound of the generated 1,671-instruction stream (5,725 SIMD "
-                        "cycles per 64 nonces at 2.39 GHz, no launch tail; tools/valu_mix2.py): the "
-                        "roofline frac is capped near 0.78 by its half-rate share, not by the kernel",
+                "what": f"measured issue bound of the {POOL_KERNEL} kernel's generated {STREAM['valu']:,}-"
+                        f"instruction stream ({STREAM_CYCLES_PER_HASH:,} SIMD cycles per 64 nonces at "
+                        f"{STREAM_CLOCK_GHZ} GHz, no launch tail; {STREAM['src']}): the roofline frac is "
+                        "capped by the stream's half-rate share (v_lshl_add_u64, v_alignbit_b32), not by "
+                        "the kernel around it",
             },
         },
         "cpu_baseline": None,

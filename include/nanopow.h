@@ -177,7 +177,9 @@ int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t 
  * of a fixed iteration count ends in a tail of one or two waves per SIMD -- and
  * iters_per_launch (default 8192) is then only the cap (and the span of bounded jobs, which
  * always complete their dense ranges).  A running launch is ended early when new jobs arrive
- * for its device.  blocks_per_cu: workgroups per CU of a search launch (default 4; 0 keeps).
+ * for its device.  Search launches use the lockstep kernel, one 1,024-lane workgroup per CU
+ * (environment NANOPOW_POOL_KERNEL=seq at npow_init selects the seq kernel instead);
+ * blocks_per_cu: 256-lane workgroups per CU of a seq-kernel search launch (default 4; 0 keeps).
  * npow_set_tuning's blocks_per_cu applies to sweeps and value ranges. */
 int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu);
 

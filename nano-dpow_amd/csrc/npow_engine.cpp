@@ -72,6 +72,10 @@ std::atomic<uint32_t> g_budget_us{20000};  // pool launches end on time, not on 
 // ~100 SGPRs admit only 6 per CU (tools/experiments/wave_probe.cpp: with 8 requested, 2 per CU start
 // only when the first 6 finish), so 4 leaves room for compiler changes.
 std::atomic<uint32_t> g_pool_blocks_per_cu{4};
+// The lockstep search kernel (npow_kernel.hip pool_body_ls) unless NANOPOW_POOL_KERNEL=seq; read
+// once, before the first launch (npow_init).
+bool g_pool_lockstep = true;
+uint32_t g_ls_lds = 0;
 
 std::vector<Device*> select_devices(uint64_t mask) {
   std::vector<Device*> out;
@@ -305,6 +309,8 @@ int npow_init(int* n_devices) try {
   // NANOPOW_VIRTUAL_DEVICES=N (testing): expose N logical devices over the physical ones
   // (logical i -> HIP device i mod n), each with its own stream, buffers and pool worker, so
   // the multi-device first-win path runs on a one-GPU machine.
+  if (const char* k = getenv("NANOPOW_POOL_KERNEL")) g_pool_lockstep = strcmp(k, "seq") != 0;
+  if (const char* l = getenv("NANOPOW_LS_LDS")) g_ls_lds = (uint32_t)atoi(l);
   int n_logical = n;
   if (const char* v = getenv("NANOPOW_VIRTUAL_DEVICES")) {
     const int k = atoi(v);
@@ -397,7 +403,7 @@ int npow_device_stats_get(int device, npow_device_stats* out) try {
   out->kernel_ms = d.kernel_ms;
   out->invalid_work = d.invalid;
   out->cus = d.cus;
-  out->grid = pool_grid_of(d);
+  out->grid = pool_shape(d).grid;
   out->clock_mhz = d.clk_ref_ticks > 0 ? d.clk_ticks / d.clk_ref_ticks * 100.0 : 0.0;
   out->host_cpu_ms = cpu - d.worker_cpu0_ms;
   out->host_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d.stats_t0).count();

@@ -75,7 +75,14 @@ extern std::atomic<uint32_t> g_budget_us;      // pool launches: wall-clock budg
 extern std::atomic<uint32_t> g_pool_blocks_per_cu;  // pool launches: workgroups per CU
 
 inline int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }        // sweep / values
-inline int pool_grid_of(const Device& d) { return d.cus * (int)g_pool_blocks_per_cu.load(); }  // searches
+// Search launches: the lockstep kernel (default) with one 1,024-lane workgroup per CU, or the
+// seq kernel with g_pool_blocks_per_cu 256-lane workgroups per CU (NANOPOW_POOL_KERNEL=seq).
+extern bool g_pool_lockstep;
+extern uint32_t g_ls_lds;  // lockstep: dynamic LDS bytes per workgroup (NANOPOW_LS_LDS)
+inline PoolShape pool_shape(const Device& d) {
+  if (g_pool_lockstep) return PoolShape{true, d.cus, g_ls_lds};
+  return PoolShape{false, d.cus * (int)g_pool_blocks_per_cu.load(), 0};
+}
 inline uint32_t poll_mask() {
   uint32_t p = g_poll.load();
   uint32_t m = 1;

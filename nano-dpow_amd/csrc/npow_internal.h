@@ -6,10 +6,13 @@
 
 #include "npow_blake2b.h"
 #include "npow_hash_asm.inc"
+#include "npow_hash_asm_lockstep.inc"
 
 namespace npow {
 
 constexpr int kBlock = 256;  // lanes per workgroup (4 waves of 64)
+constexpr int kLsWaves = 16;                // lockstep pool kernel: waves per workgroup (4 per SIMD) ...
+constexpr int kLsBlock = kLsWaves * 64;     // ... one workgroup per CU
 
 enum class Mode : int { kSweep = 1, kValues = 2 };  // npow_task_kernel (first-win search: npow_pool_kernel)
 
@@ -159,15 +162,31 @@ struct PoolMailbox {
   alignas(64) PoolClk clk[4][kClkWaves];  // [launch ring][XCD] (host: kEventRing == 4)
 };
 
+// Grid of a search launch.  A "unit" is what an entry's share is counted in: a wave (seq kernel)
+// or a workgroup of kLsWaves waves (lockstep kernel, whose workgroups work on one entry at a time).
+struct PoolShape {
+  bool lockstep;  // npow_pool_kernel_ls* (1,024-lane workgroups) instead of npow_pool_kernel*
+  int grid;       // workgroups
+  uint32_t lds;   // lockstep: dynamic LDS bytes per workgroup (> half a CU's keeps one per CU)
+  uint32_t units() const { return lockstep ? (uint32_t)grid : (uint32_t)grid * (kBlock / 64); }
+  uint32_t waves_per_unit() const { return lockstep ? (uint32_t)kLsWaves : 1u; }
+  // nonces a bounded entry e of n can cover in one launch of `iters` wave iterations
+  uint64_t own(uint32_t e, uint32_t n, uint32_t iters) const {
+    const uint32_t U = units();
+    return (uint64_t)(U / n + (e < U % n ? 1u : 0u)) * waves_per_unit() * iters * 64;
+  }
+  uint64_t full(uint32_t iters) const { return (uint64_t)units() * waves_per_unit() * iters * 64; }
+};
+
 // Launchers (defined in npow_kernel.hip).
 hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs& a, DevState* st,
                        HostMailbox* mb, uint64_t* out);
 // bounded: the table holds a bounded entry (selects the kernel variant with per-lane range tests)
-hipError_t launch_pool(int grid, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
+hipError_t launch_pool(const PoolShape& sh, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
                        PoolMailbox* mb);
 // The same with the table (n <= kArgEntries) passed in the kernel arguments: no upload.
-hipError_t launch_pool_arg(int grid, hipStream_t stream, const PoolTable& host_tab, bool bounded, PoolDevState* st,
-                           PoolMailbox* mb);
+hipError_t launch_pool_arg(const PoolShape& sh, hipStream_t stream, const PoolTable& host_tab, bool bounded,
+                           PoolDevState* st, PoolMailbox* mb);
 // Fill a.u[] for one root (host).
 inline void fill_uniforms(LaunchArgs& a, const RootPrecomp& pre) { npow_asm_uniforms(pre.m, a.u); }
 

@@ -438,6 +438,172 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
 #endif
 }
 
+// ---- Lockstep pool body (npow_pool_kernel_ls*) ---------------------------------------------
+// The same search with the lockstep instruction stream (npow_hash_asm_lockstep.inc): one
+// 1,024-lane workgroup per CU puts 4 waves on every SIMD, all of one workgroup, and the
+// stream's s_barrier after every interval (the full-rate part of one G step, then the
+// half-rate part of the next) keeps them in the same phase -- full-rate and half-rate runs of
+// different waves then no longer mix on the SIMD (5,251 vs 6,139 SIMD
+// cycles per hash in tools/experiments/stream_lockstep.py).  Every wave of a workgroup must
+// therefore hash the same number of times, so everything that ends a wave's loop is decided
+// per workgroup:
+//  * a workgroup works on one entry at a time (entry g % n first; bounded entries are dense
+//    over their own workgroups' waves, PoolEntry comment with unit = workgroup);
+//  * a wave that wants its workgroup to stop (a win, a dead / killed / yielded entry, the time
+//    budget) files a request in LDS, s_stop[segment % 3] = min((it + 1) << 1 | kind) with
+//    kind 0 = end the launch, 1 = leave the entry; every wave reads the word at the top of an
+//    iteration and obeys only requests filed at least one full hash earlier (value < it at the
+//    top): those lie behind the hash's barriers for every wave, so all waves reach the same
+//    verdict in the same iteration (two iterations after the request, ~4 us);
+//  * leaving an entry: wave 0 picks the next live unbounded entry and broadcasts it through
+//    LDS (one __syncthreads); each entry segment has its own request word (3 rotate: the word
+//    of segment s + 1 is reset at the end of segment s, after its last reader, segment s - 2).
+__device__ __forceinline__ void pool_load_ls(const PoolEntry* __restrict__ pe, PoolCursor& c, uint32_t g, uint32_t wv,
+                                             uint32_t G, uint32_t n, uint32_t e, uint32_t iters) {
+#pragma unroll
+  for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) c.u[i] = pe->u[i];
+  c.threshold = pe->threshold;
+  c.base = pe->base;
+  c.gen = pe->gen;
+  c.slot = pe->slot;
+  c.bounded = pe->bounded;
+  if (pe->bounded) {
+    // own workgroups only: rank r = g / n of cnt; count <= K * iters * 64 (host: launch())
+    const uint32_t cnt = G / n + (e < G % n ? 1u : 0u);
+    const uint32_t j0 = (g / n) * kLsWaves;
+    c.K = kLsWaves * cnt;
+    c.j = j0 + wv;
+    const uint32_t blocks = (uint32_t)((pe->count + 63) / 64);
+    c.it_end = blocks > j0 ? (blocks - j0 + c.K - 1) / c.K : 0u;  // the workgroup's first wave's count
+    c.last_b = blocks - 1u;
+    c.tail = (uint32_t)(pe->count - (uint64_t)(blocks - 1u) * 64);
+  } else {
+    c.K = G * kLsWaves;
+    c.j = g * kLsWaves + wv;
+    c.it_end = iters;
+    c.last_b = 0xffffffffu;
+    c.tail = 64;
+  }
+}
+
+__device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+template <bool BOUNDED>
+__device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
+                                             PoolMailbox* __restrict__ mb, const uint64_t t_start) {
+  __shared__ uint32_t s_stop[3];  // per entry segment (mod 3): the earliest stop request
+  __shared__ uint32_t s_next;     // wave 0's choice of the next entry
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = blockIdx.x, G = gridDim.x;
+  const uint32_t w = g * kLsWaves + wv;
+  const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask, budget = tab->budget;
+  const uint64_t yield_base = tab->yield_base;
+  unsigned long long* const done_base = &st->done[0][(w % kPoolDoneShards) * 8];
+  if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
+  __syncthreads();
+
+  uint32_t e = g % n, seg = 0;
+  PoolCursor c;
+  pool_load_ls(&tab->e[e], c, g, wv, G, n, e, iters);
+  uint32_t it = 0;
+  bool end = false;
+  for (;;) {
+    uint32_t done = 0;
+    uint32_t* const req_word = &s_stop[seg % 3];
+    while (it < c.it_end) {
+      const uint32_t verdict = *(volatile uint32_t*)req_word;  // consumed after the hash
+      const uint64_t dead = load_dead(st, c.slot);
+      const bool poll = ((it + w) & poll_mask) == 0;
+      uint64_t kill, yld;
+      if (__builtin_expect(poll, 0)) {
+        kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        yld = __hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
+      const uint32_t it0 = it;
+      const uint32_t b = it * c.K + c.j;
+      const uint64_t nonce = c.base + ((uint64_t)b << 6) + lane;
+      const uint64_t value = npow_asm_work_value_lockstep(nonce, c.u);
+      ++it;
+      bool hit = value >= c.threshold;
+      if constexpr (BOUNDED) {
+        const uint32_t in_lanes = b < c.last_b ? 64u : (b == c.last_b ? c.tail : 0u);
+        hit = hit && lane < in_lanes;
+        done += in_lanes;
+      } else {
+        done += 64;
+      }
+      uint32_t req = 0;  // 1: leave the entry, 2: end the launch
+      const uint64_t hits = __ballot(hit);
+      if (__builtin_expect(hits != 0, 0)) {
+        const int wl = __builtin_ctzll(hits);
+        const uint64_t wn = readlane64(nonce, wl), wval = readlane64(value, wl);
+        if (lane == 0) {
+          if (atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen) < c.gen) {  // first win
+            PoolWin* pw = &mb->win[c.slot];
+            __hip_atomic_store(&pw->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&pw->value, wval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_store(&pw->gen, c.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+          }
+        }
+        req = 1;
+      }
+      if (__builtin_expect(poll, 0)) {
+        if (readlane64(yld, 0) != yield_base) {  // new jobs wait: end every unbounded entry (pool_body)
+          if (lane == 0)
+            for (uint32_t k = 0; k < n; ++k)
+              if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
+          if (!c.bounded) req = 1;
+        }
+        if (readlane64(kill, 0) == c.gen) {
+          if (lane == 0) atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen);  // relay
+          req = 1;
+        }
+      }
+      if (readlane64(dead, 0) == c.gen) req = 1;
+      if (budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget) req = 2;
+      if (__builtin_expect(req != 0, 0)) {
+        if (lane == 0) atomicMin(req_word, (it << 1) | (req == 1 ? 1u : 0u));
+        lds_drain();  // complete before the next hash's first barrier
+      }
+      // the word as read before this hash: requests with value < it0 were filed at the end of
+      // iteration it0 - 2 or earlier, behind the previous hash's barriers, so every wave saw
+      // them (a later one, value it0, some waves may have seen: all ignore it) -- one verdict
+      if ((__builtin_amdgcn_readfirstlane(verdict) >> 1) < it0) {
+        end = (__builtin_amdgcn_readfirstlane(verdict) & 1) == 0;
+        break;
+      }
+    }
+    if (lane == 0 && done) atomicAdd(done_base + (size_t)c.slot * (kPoolDoneShards * 8), (unsigned long long)done);
+    if (it >= iters || end) break;
+    // leave the entry (its bounded range is used up, or a request): wave 0 picks the next live
+    // unbounded entry, cyclic from e + 1, and resets the request word of the next segment
+    if (wv == 0) {
+      uint32_t next = n;
+      for (uint32_t k = 1; k < n; ++k) {
+        uint32_t e2 = e + k;
+        if (e2 >= n) e2 -= n;
+        const PoolEntry* pe = &tab->e[e2];
+        if (pe->bounded) continue;
+        if (load_dead(st, pe->slot) >= pe->gen) continue;
+        next = e2;
+        break;
+      }
+      if (lane == 0) {
+        s_next = next;
+        s_stop[(seg + 1) % 3] = ~0u;
+      }
+    }
+    __syncthreads();
+    const uint32_t next = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_next);
+    if (next == n) break;
+    e = next;
+    ++seg;
+    pool_load_ls(&tab->e[e], c, g, wv, G, n, e, iters);
+  }
+}
+
 // Live in-kernel clock (PoolClk): the first wave of workgroups 0..kClkWaves-1 -- one per XCD,
 // workgroups are dealt to XCDs round-robin -- reads s_memtime after its first instruction and
 // both counters after its last; 2 scalar reads and one 24-byte store per 4,096 waves.
@@ -489,24 +655,61 @@ void npow_pool_kernel_arg(const PoolTableArg targ, PoolDevState* __restrict__ st
   clk_end(tab, mb, t_start, c_start);
 }
 
-hipError_t launch_pool(int grid, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
+// The lockstep variants: 1,024-lane workgroups, one per CU (pool_body_ls).
+template <bool BOUNDED>
+__global__ __launch_bounds__(kLsBlock) void npow_pool_kernel_ls(const PoolTable* __restrict__ tab,
+                                                               PoolDevState* __restrict__ st,
+                                                               PoolMailbox* __restrict__ mb) {
+  uint64_t t_start;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
+  const uint64_t c_start = clk_begin();
+  pool_body_ls<BOUNDED>(tab, st, mb, t_start);
+  clk_end(tab, mb, t_start, c_start);
+}
+
+template <bool BOUNDED>
+__global__ __launch_bounds__(kLsBlock) void npow_pool_kernel_ls_arg(const PoolTableArg targ,
+                                                                   PoolDevState* __restrict__ st,
+                                                                   PoolMailbox* __restrict__ mb) {
+  uint64_t t_start;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
+  (void)targ;
+  const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();
+  const uint64_t c_start = clk_begin();
+  pool_body_ls<BOUNDED>(tab, st, mb, t_start);
+  clk_end(tab, mb, t_start, c_start);
+}
+
+hipError_t launch_pool(const PoolShape& sh, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
                        PoolMailbox* mb) {
-  if (bounded)
-    npow_pool_kernel<true><<<grid, kBlock, 0, stream>>>(tab, st, mb);
-  else
-    npow_pool_kernel<false><<<grid, kBlock, 0, stream>>>(tab, st, mb);
+  if (sh.lockstep) {
+    if (bounded)
+      npow_pool_kernel_ls<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
+    else
+      npow_pool_kernel_ls<false><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
+  } else if (bounded) {
+    npow_pool_kernel<true><<<sh.grid, kBlock, 0, stream>>>(tab, st, mb);
+  } else {
+    npow_pool_kernel<false><<<sh.grid, kBlock, 0, stream>>>(tab, st, mb);
+  }
   return hipGetLastError();
 }
 
-hipError_t launch_pool_arg(int grid, hipStream_t stream, const PoolTable& host_tab, bool bounded, PoolDevState* st,
-                           PoolMailbox* mb) {
+hipError_t launch_pool_arg(const PoolShape& sh, hipStream_t stream, const PoolTable& host_tab, bool bounded,
+                           PoolDevState* st, PoolMailbox* mb) {
   if (host_tab.n > (uint32_t)kArgEntries) return hipErrorInvalidValue;
   PoolTableArg a;
   memcpy(&a, &host_tab, pool_table_bytes(host_tab.n));
-  if (bounded)
-    npow_pool_kernel_arg<true><<<grid, kBlock, 0, stream>>>(a, st, mb);
-  else
-    npow_pool_kernel_arg<false><<<grid, kBlock, 0, stream>>>(a, st, mb);
+  if (sh.lockstep) {
+    if (bounded)
+      npow_pool_kernel_ls_arg<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
+    else
+      npow_pool_kernel_ls_arg<false><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
+  } else if (bounded) {
+    npow_pool_kernel_arg<true><<<sh.grid, kBlock, 0, stream>>>(a, st, mb);
+  } else {
+    npow_pool_kernel_arg<false><<<sh.grid, kBlock, 0, stream>>>(a, st, mb);
+  }
   return hipGetLastError();
 }
 

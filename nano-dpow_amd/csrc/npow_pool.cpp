@@ -507,7 +507,7 @@ int Worker::launch() {
           (double)g_budget_us.load() - kPrelaunchUs)
     return NPOW_OK;
   const uint32_t iters = g_iters.load();
-  const uint32_t W = (uint32_t)pool_grid_of(d_) * (kBlock / 64);
+  const PoolShape sh = pool_shape(d_);
   PoolTable& t = *d_.h_tab[ring_];
   uint32_t n = 0;
   bool bounded = false;
@@ -537,8 +537,8 @@ int Worker::launch() {
       // densely; an unbounded job claims a full launch region (W * iters * 64, holes allowed)
       // unless less than that is left, which then becomes a dense bounded entry too
       std::deque<Range>& todo = j.todo[sl.k];
-      const uint64_t own = (uint64_t)(W / n + (e < W % n ? 1u : 0u)) * iters * 64;
-      const uint64_t full = (uint64_t)W * iters * 64;
+      const uint64_t own = sh.own(e, n, iters);
+      const uint64_t full = sh.full(iters);
       if (todo.empty()) todo.push_back({j.start, 0});  // cannot happen (adopt / no_more); an empty entry
       Range& r = todo.front();
       const uint64_t want = j.max_per_dev ? own : full;
@@ -569,11 +569,11 @@ int Worker::launch() {
     return fail(NPOW_ERR_HIP, "injected launch failure (NANOPOW_FAULT_HIP)");
   if (n <= (uint32_t)kArgEntries && !force_upload) {  // the table rides in the kernel arguments
     HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
-    HIPTRY(launch_pool_arg(pool_grid_of(d_), d_.stream, t, bounded, d_.pst, d_.pmb_dev));
+    HIPTRY(launch_pool_arg(sh, d_.stream, t, bounded, d_.pst, d_.pmb_dev));
   } else {
     HIPTRY(hipMemcpyAsync(d_.d_tab[r], d_.h_tab[r], bytes, hipMemcpyHostToDevice, d_.stream));
     HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
-    HIPTRY(launch_pool(pool_grid_of(d_), d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
+    HIPTRY(launch_pool(sh, d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
   }
   HIPTRY(hipEventRecord(d_.ev_stop[r], d_.stream));
   if (q_.empty()) front_start_ = std::chrono::steady_clock::now();

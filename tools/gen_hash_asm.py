@@ -290,6 +290,8 @@ VOP3_SIMPLE = True
 # rotr32 as two in-place xors + two v_mov_b32 into the fresh pair (movs issue nearly free)
 SWAP_MOV = False
 LAT = 8.0
+ZPAIRS = 2  # {t, 0} pairs of the rotl1 trick in use at once (lockstep: one per G of a half-round, +2)
+BARRIER_LINES = ["s_barrier"]  # --sched lockstep: what ends an interval (+ "s_nop 0" keeps 8-byte parity)
 
 
 def op_cost(op: Op) -> float:
@@ -347,6 +349,65 @@ def schedule(ops: List[Op], mode: str) -> List[Op]:
     return order
 
 
+def schedule_lockstep(ops: List[Op], shift: bool = False, pad_end: bool = False) -> list:
+    """--sched lockstep: the 4 independent G functions of each half-round advance together through
+    intervals, each interval = the full-rate part of one G step for all of them (xors, the rotl1
+    shift) followed by the half-rate part of the next (64-bit adds, alignbits, the rotl1 add), and
+    an s_barrier ends every interval.  In a workgroup of 4 waves per SIMD the barrier keeps the
+    SIMD's waves in the same phase (tools/experiments/phase_lockstep.py: hash-shaped intervals cost
+    ~3.0 cycles per instruction with barriers, 3.7 without).  Returns items for emit(): ops, (op,
+    "F") / (op, "H") halves of a split rotation, and "BARRIER".
+
+    shift: the anti-phase stream -- every interval's half-rate part moves to the front of the next
+    interval, so an interval is (H of step i-1, F of step i): run beside the unshifted stream on the
+    other waves of a SIMD, full-rate and half-rate runs overlap.  It has one more interval than the
+    unshifted stream; pad_end gives the unshifted one a trailing barrier so the counts match."""
+    by_g: Dict[int, List[Op]] = {}
+    for op in ops:
+        by_g.setdefault(op.g, []).append(op)
+    key: Dict[Tuple[int, str], Tuple[int, int]] = {}   # (op id, part) -> (interval, 0 = F / 1 = H)
+    for g, gops in by_g.items():
+        L = 0
+        base = 4 * (g // 4)  # 4 intervals per half-round
+        for op in gops:
+            if op.kind == "add":
+                key[(op.id, "all")] = (base + L, 1)
+            elif op.kind == "xrot32":
+                L += 1
+                key[(op.id, "all")] = (base + L, 0)
+            elif op.kind == "xrot":
+                L += 1
+                key[(op.id, "F")] = (base + L, 0)
+                key[(op.id, "H")] = (base + L, 1)
+            else:  # the output xor
+                key[(op.id, "all")] = (base + L + 1, 0)
+    # dependencies win over the pattern: an op is never placed before what it reads
+    done: Dict[int, Tuple[int, int]] = {}
+    for op in ops:  # topological
+        parts = ["F", "H"] if (op.id, "F") in key else ["all"]
+        lo = max((done[p.id] for p in op.preds), default=(0, 0))
+        prev = lo
+        for part in parts:
+            k = max(key[(op.id, part)], prev)
+            key[(op.id, part)] = k
+            prev = k
+        done[op.id] = prev
+    if shift:  # (iv, F) -> (iv, 2nd); (iv, H) -> (iv + 1, 1st): monotone, so dependencies still hold
+        key = {k: (iv + ph, 1 - ph) for k, (iv, ph) in key.items()}
+    units = sorted(key.items(), key=lambda kv: (kv[1][0], kv[1][1], kv[0][0]))
+    idx = {op.id: op for op in ops}
+    items: list = []
+    cur = None
+    for (oid, part), (iv, _ph) in units:
+        if cur is not None and iv != cur:
+            items.append("BARRIER")
+        cur = iv
+        items.append((idx[oid], part) if part != "all" else idx[oid])
+    if pad_end:
+        items.append("BARRIER")
+    return items
+
+
 # ---------------------------------------------------------------------------------------
 # Register allocation + emission
 class Alloc:
@@ -382,7 +443,10 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
     uni_index = {n.id: i for i, n in enumerate(frontier)}
     # remaining-use counters per lane-varying node (64-bit), counting each op read once
     remaining: Dict[int, int] = {}
-    for op in order:
+    for item in order:
+        if isinstance(item, str) or (isinstance(item, tuple) and item[1] == "H"):
+            continue  # barriers; a split op's sources are read by its F part
+        op = item[0] if isinstance(item, tuple) else item
         for s in op.srcs:
             if not s.uniform:
                 remaining[s.id] = remaining.get(s.id, 0) + 1
@@ -392,7 +456,7 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
     zpairs = []
     lines_pre: List[str] = []
     if ROTL1_VIA_ADD and not ROTL1_CC:
-        for _ in range(2):
+        for _ in range(ZPAIRS):
             r = al.take2()
             zpairs.append(r)
             lines_pre.append(f"v_mov_b32 v{r + 1}, 0")
@@ -454,7 +518,12 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
         # b must be in a VGPR: nonce or lane-varying
         return half(a, hi), half(b, hi)
 
-    for op in order:
+    pend: Dict[int, Tuple[int, int]] = {}  # split xrot ops (--sched lockstep): temps between F and H parts
+    for item in order:
+        if isinstance(item, str):  # "BARRIER": the end of a lockstep interval
+            lines.extend(BARRIER_LINES)
+            continue
+        op, part = item if isinstance(item, tuple) else (item, "all")
         a, b = op.srcs
         if op.kind == "add":
             if a.uniform and b.uniform:
@@ -545,6 +614,11 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             cnt("v_addc_co_u32")
             cnt("v_addc_co_u32")
         elif op.kind == "xrot" and op.n == 63 and ROTL1_VIA_ADD:
+            if part == "H":  # second half of a split op: x << 1 + {x >> 63, 0}
+                r, z = pend.pop(op.id)
+                lines.append(f"v_lshl_add_u64 v[{r}:{r + 1}], v[{r}:{r + 1}], 1, v[{z}:{z + 1}]")
+                cnt("v_lshl_add_u64")
+                continue
             s0l, s1l = xor_operands(a, b, 0)
             s0h, s1h = xor_operands(a, b, 1)
             consume(op)
@@ -554,26 +628,35 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
             z = zpairs[zturn[0] % len(zpairs)]
             zturn[0] += 1
             lines.append(f"v_lshrrev_b32 v{z}, 31, v{r + 1}")
-            lines.append(f"v_lshl_add_u64 v[{r}:{r + 1}], v[{r}:{r + 1}], 1, v[{z}:{z + 1}]")
             loc[op.dst.id] = r
             cnt("v_xor_b32")
             cnt("v_xor_b32")
             cnt("v_lshrrev_b32")
+            if part == "F":
+                pend[op.id] = (r, z)
+                continue
+            lines.append(f"v_lshl_add_u64 v[{r}:{r + 1}], v[{r}:{r + 1}], 1, v[{z}:{z + 1}]")
             cnt("v_lshl_add_u64")
         elif op.kind == "xrot":
-            s0l, s1l = xor_operands(a, b, 0)
-            s0h, s1h = xor_operands(a, b, 1)
-            hi_regs = tuple(loc[x.id] + 1 for x in (a, b) if x.id in loc)
-            consume(op)
-            tl = al.take1(avoid=hi_regs)   # written before the hi halves are read
-            th = al.take1(avoid=(tl,))
-            lines.append(f"v_xor_b32 v{tl}, {s0l}, {s1l}")
-            lines.append(f"v_xor_b32 v{th}, {s0h}, {s1h}")
+            if part == "H":
+                tl, th = pend.pop(op.id)
+            else:
+                s0l, s1l = xor_operands(a, b, 0)
+                s0h, s1h = xor_operands(a, b, 1)
+                hi_regs = tuple(loc[x.id] + 1 for x in (a, b) if x.id in loc)
+                consume(op)
+                tl = al.take1(avoid=hi_regs)   # written before the hi halves are read
+                th = al.take1(avoid=(tl,))
+                lines.append(f"v_xor_b32 v{tl}, {s0l}, {s1l}")
+                lines.append(f"v_xor_b32 v{th}, {s0h}, {s1h}")
+                cnt("v_xor_b32")
+                cnt("v_xor_b32")
+                if part == "F":
+                    pend[op.id] = (tl, th)
+                    continue
             r = al.take2(avoid=(tl, th))
             loc[op.dst.id] = r
             n = op.n
-            cnt("v_xor_b32")
-            cnt("v_xor_b32")
             # half h of rotr_n: (x_h >> n) | (x_other << (32 - n)) -- one v_alignbit_b32, or
             # v_lshrrev_b32 + v_mad_u32_u24 (x_other[23:0] * 2^(32-n) + (x_h >> n); exact for
             # n = 16, 24), which runs in the multiplier next to alignbit / v_lshl_add_u64
@@ -613,6 +696,9 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
     if VOP3_SIMPLE:
         conv = []
         for ln in out_lines:
+            if " " not in ln:  # s_barrier
+                conv.append(ln)
+                continue
             opc, rest = ln.split(" ", 1)
             if opc in ("v_xor_b32", "v_lshrrev_b32") and "0x" not in rest:
                 opc += "_e64"
@@ -866,10 +952,10 @@ def fuse_output_xor(lines: List[str], counts: Dict[str, int]) -> List[str]:
     out = list(lines)
 
     def dst(ln):
-        return ln.split(" ", 1)[1].split(",")[0].strip()
+        return ln.split(" ", 1)[1].split(",")[0].strip() if " " in ln else ""
 
     def srcs(ln):
-        return [t.strip().split(" ")[0] for t in ln.split(" ", 1)[1].split(",")[1:]]
+        return [t.strip().split(" ")[0] for t in ln.split(" ", 1)[1].split(",")[1:]] if " " in ln else []
 
     for half, name in ((0, "value_lo"), (1, "value_hi")):
         k = next((i for i, ln in enumerate(out) if ln.startswith("v_xor_b32 ") and dst(ln) == f"%[{name}]"), None)
@@ -940,8 +1026,8 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
 
     carry: Dict[str, int] = {}  # "vcc" or "s[k:k+1]" -> the carry bit it holds
     for ln in lines:
-        if ln.startswith(".") or ln.startswith("s_nop"):
-            continue  # placement directives / padding
+        if ln.startswith(".") or ln.startswith("s_nop") or ln.startswith("s_barrier"):
+            continue  # placement directives / padding / lockstep interval ends
         opc, rest = ln.split(" ", 1)
         opc = opc[:-4] if opc.endswith("_e64") else opc
         ops = [t.strip() for t in rest.split(",")]
@@ -1031,7 +1117,10 @@ PAD = ['.p2align 3', 's_nop 0']
 
 
 def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List[str], vbase: int, vmax: int,
-              counts: Dict[str, int], sched: str, est_cycles: float) -> None:
+              counts: Dict[str, int], sched: str, est_cycles: float, func: str = "npow_asm_work_value") -> None:
+    """The .inc: the host uniform program and the device function.  A second stream of the same
+    hash (func != npow_asm_work_value) is device-only: it reads the same uniforms (the frontier does
+    not depend on the schedule) and is included after the primary one."""
     nu = len(frontier)
     clobbers = ", ".join(f'"v{r}"' for r in range(vbase, vmax))
     text = "\n".join(lines)
@@ -1055,14 +1144,9 @@ def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List
     uni_ops = ",\n        ".join(ops_in)
     body = "\n".join(f'      "{ln}\\n"' for ln in PAD + lines)
     cnt_txt = ", ".join(f"{k} {v}" for k, v in sorted(counts.items()))
-    txt = f"""// GENERATED by tools/gen_hash_asm.py (--sched {sched}) -- do not edit by hand.
-//
-// gfx950 instruction stream of the Nano work value for one nonce per lane:
-//   value = BLAKE2b-64(LE64(nonce) || root)   (nano-work-server.exe @1661643 nano_work)
-// Per nonce: {sum(counts.values())} VALU instructions ({cnt_txt});
-// VGPR window v{vbase}..v{vmax - 1}; {nu} uniform 64-bit values, {len(ops_in)} asm input operands;
-// modelled issue cost {est_cycles:.0f} SIMD cycles per wave (64 nonces).
-#pragma once
+    n_bar = sum(1 for ln in lines if ln.startswith("s_barrier"))
+    if func == "npow_asm_work_value":
+        prologue = f"""#pragma once
 #include <stdint.h>
 
 #define NPOW_ASM_N_UNIFORMS {nu}
@@ -1071,11 +1155,30 @@ def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List
 static inline void npow_asm_uniforms(const uint64_t m[4], uint64_t u[NPOW_ASM_N_UNIFORMS]) {{
 {chr(10).join('  ' + s for s in host_prog)}
 }}
+"""
+    else:
+        prologue = f"""#pragma once
+#include <stdint.h>
 
-__device__ __forceinline__ uint64_t npow_asm_work_value(uint64_t nonce, const uint64_t (&u)[NPOW_ASM_N_UNIFORMS]) {{
+static_assert(NPOW_ASM_N_UNIFORMS == {nu}, "include after the primary stream: the same uniforms");
+"""
+    if n_bar:
+        prologue += f"""
+// {n_bar} s_barrier: every wave of the workgroup must run this function the same number of
+// times, in workgroup-uniform control flow (asm volatile: kept even when a value is unused).
+"""
+    txt = f"""// GENERATED by tools/gen_hash_asm.py (--sched {sched}) -- do not edit by hand.
+//
+// gfx950 instruction stream of the Nano work value for one nonce per lane:
+//   value = BLAKE2b-64(LE64(nonce) || root)   (nano-work-server.exe @1661643 nano_work)
+// Per nonce: {sum(counts.values())} VALU instructions ({cnt_txt});
+// VGPR window v{vbase}..v{vmax - 1}; {nu} uniform 64-bit values, {len(ops_in)} asm input operands;
+// modelled issue cost {est_cycles:.0f} SIMD cycles per wave (64 nonces).
+{prologue}
+__device__ __forceinline__ uint64_t {func}(uint64_t nonce, const uint64_t (&u)[NPOW_ASM_N_UNIFORMS]) {{
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t value_lo, value_hi;
-  asm(
+  asm{" volatile" if n_bar else ""}(
 {body}
       : [value_lo] "=&v"(value_lo), [value_hi] "=&v"(value_hi)
       : {uni_ops}
@@ -1093,7 +1196,15 @@ __device__ __forceinline__ uint64_t npow_asm_work_value(uint64_t nonce, const ui
 
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--sched", default="seq", choices=["rr", "cp", "seq", "ilp"])
+    ap.add_argument("--sched", default="seq", choices=["rr", "cp", "seq", "ilp", "lockstep"])
+    ap.add_argument("--barrier-nop", action="store_true",
+                    help="lockstep: an s_nop 0 after each s_barrier (keeps 8-byte instruction parity)")
+    ap.add_argument("--barrier-every", type=int, default=1,
+                    help="lockstep: an s_barrier after every N-th interval (0 = none; experiments)")
+    ap.add_argument("--func", default="npow_asm_work_value",
+                    help="device function name; any other name writes a device-only second stream (write_inc)")
+    ap.add_argument("--shift", action="store_true", help="lockstep: the anti-phase stream (schedule_lockstep)")
+    ap.add_argument("--pad-end", action="store_true", help="lockstep: a trailing s_barrier (pairs with --shift)")
     ap.add_argument("--lat", type=float, default=8.0, help="ilp: result latency (SIMD cycles)")
     ap.add_argument("--window", type=int, default=48, help="ilp: scheduling window (instructions)")
     ap.add_argument("--base", type=int, default=16, help="first VGPR of the clobbered window")
@@ -1142,7 +1253,24 @@ def main() -> int:
         order_i = schedule_ilp(ins, args.lat, args.window)
         lines, vmax, counts = allocate_and_emit(order_i, vrs, args.base, args.limit, VOP3_SIMPLE)
     else:
-        order = schedule(ops, args.sched)
+        if args.sched == "lockstep":
+            global ZPAIRS, BARRIER_LINES
+            ZPAIRS = 6
+            BARRIER_LINES = ["s_barrier", "s_nop 0"] if args.barrier_nop else ["s_barrier"]
+            for op in reversed(ops):  # priorities are unused, but keep op.prio defined
+                op.prio = 0.0
+            order = schedule_lockstep(ops, args.shift, args.pad_end)
+            if args.barrier_every != 1:  # experiments: thin out the barriers
+                kept, k = [], 0
+                for it in order:
+                    if it == "BARRIER":
+                        k += 1
+                        if args.barrier_every == 0 or k % args.barrier_every:
+                            continue
+                    kept.append(it)
+                order = kept
+        else:
+            order = schedule(ops, args.sched)
         lines, _uni, vmax, counts = emit(order, frontier, out, args.base, args.limit)
     if args.fuse_out == "bitop3":
         lines = fuse_output_xor(lines, counts)
@@ -1154,6 +1282,8 @@ def main() -> int:
             src0 = ln.split(",")[1].strip()
             est += COST["v_xor_b32_k"] if src0.startswith("0x") else (
                 COST["v_xor_b32_s"] if src0.startswith("%[u") else COST["v_xor_b32"])
+        elif opc.startswith("s_"):
+            continue  # s_barrier / s_nop: not VALU issue
         else:
             est += COST[opc]
     rng = random.Random(2024)
@@ -1171,7 +1301,8 @@ def main() -> int:
     write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --add {args.add} --enc {args.enc}"
               + (f" --rotmad {args.rotmad}" if args.rotmad != "none" else "") + (" --swapmov" if args.swapmov else "")
               + (f" --lat {args.lat:g} --window {args.window}" if args.sched == "ilp" else "") + f" --pad {args.pad}"
-              + (" --fuse-out none" if args.fuse_out == "none" else ""), est)
+              + (" --fuse-out none" if args.fuse_out == "none" else "")
+              + (f" --func {args.func}" if args.func != "npow_asm_work_value" else ""), est, args.func)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
           f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")
     return 0

@@ -42,6 +42,13 @@ PATTERNS = {
     "align mov xor": ["align", "mov", "xor"], "align mov e64 xor": ["align", "mov3", "xor"],
     "add64 mov xor": ["add64", "mov", "xor"], "add64 xor": ["add64", "xor"],
     "align mov mov xor": ["align", "mov", "mov", "xor"], "xor align mov": ["xor", "align", "mov"],
+    # long runs of one class per wave (round 2): do waves in different phases overlap the classes?
+    "xor x16|align x16": ["xor"] * 16 + ["align"] * 16, "xor x32|align x32": ["xor"] * 32 + ["align"] * 32,
+    "xor x64|align x64": ["xor"] * 64 + ["align"] * 64, "xor x128|align x128": ["xor"] * 128 + ["align"] * 128,
+    "xor x32|add64 x32": ["xor"] * 32 + ["add64"] * 32, "xor x64|add64 x64": ["xor"] * 64 + ["add64"] * 64,
+    "x8 a8 d4 (4 G lockstep)": ["xor"] * 8 + ["align"] * 8 + ["add64"] * 4,
+    "x16 a16 d8 (8 G lockstep)": ["xor"] * 16 + ["align"] * 16 + ["add64"] * 8,
+    "x32 a32 d16 (16 G lockstep)": ["xor"] * 32 + ["align"] * 32 + ["add64"] * 16,
     "lshl": ["lshl"], "or": ["or"], "lshr64": ["lshr64"], "add3": ["add3"], "addu": ["addu"],
     "xor|alignbyte alt": ["xor", "alignbyte"], "xor|lshlor alt": ["xor", "lshlor"],
     "xor xor|addco addc": ["xor", "xor", "addco", "addc"],
@@ -199,7 +206,7 @@ def real_stream(path=None):
 def main():
     bpc = int(sys.argv[1]) if len(sys.argv) > 1 else 4
     budget_us = int(sys.argv[2]) if len(sys.argv) > 2 else 5000
-    n_body = 360
+    n_body = int(os.environ.get("MIX_NBODY", "360"))
     clob = ", ".join(f'"v{r}"' for r in range(8, 64))
     sclob = ", ".join(f'"s{r}"' for r in range(36, 70))
     cclob = ", ".join(f'"s{r}"' for r in range(20, 32))  # carry pairs of the SGPR-carry patterns / streams
