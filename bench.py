@@ -84,14 +84,15 @@ SEND = 0xfffffff800000000
 OPS_PER_NONCE = 2232                # int32 VALU ops of one 12-round compression
 PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # MI355X: 256 CU x (4 SIMD x 32 lanes) x 2.4 GHz = 78.6 Tops/s
 # The instruction stream's own issue bound (informational, next to the roofline), per search kernel:
-#  * lockstep (default): the barrier-interval stream, 1,675 VALU instructions, 5,251 SIMD cycles per
-#    wave (64 nonces) with one 1,024-lane workgroup per CU and no launch tail
-#    (tools/experiments/stream_lockstep.py, profiles/r02_stream_lockstep.jsonl), 3.135 cycles each;
+#  * lockstep (default): the barrier-interval stream with VOP2 xors and shifts, 1,677 VALU
+#    instructions, 5,044 SIMD cycles per wave (64 nonces) with one 1,024-lane workgroup per CU and
+#    no launch tail (tools/experiments/stream_lockstep.py, profiles/r02_lockstep_stream_variants.jsonl
+#    "vop2"), 3.008 cycles each;
 #  * seq (NANOPOW_POOL_KERNEL=seq): 1,671 instructions at 5,725 cycles, time-budgeted, every SIMD
 #    saturated (tools/valu_mix2.py "real hash stream": profiles/r01_valu_mix2_final_stream.jsonl).
 POOL_KERNEL = "seq" if os.environ.get("NANOPOW_POOL_KERNEL") == "seq" else "lockstep"
-STREAM = {"lockstep": {"cycles": 5251, "valu": 1675, "kernel": "npow_pool_kernel_ls_arg<false>",
-                       "src": "tools/experiments/stream_lockstep.py, profiles/r02_stream_lockstep.jsonl"},
+STREAM = {"lockstep": {"cycles": 5044, "valu": 1677, "kernel": "npow_pool_kernel_ls_arg<false>",
+                       "src": "tools/experiments/stream_lockstep.py, profiles/r02_lockstep_stream_variants.jsonl"},
           "seq": {"cycles": 5725, "valu": 1671, "kernel": "npow_pool_kernel_arg<false>",
                   "src": "tools/valu_mix2.py, profiles/r01_valu_mix2_final_stream.jsonl"}}[POOL_KERNEL]
 STREAM_CYCLES_PER_HASH = STREAM["cycles"]

@@ -109,7 +109,10 @@ struct Inflight {
 // Launch one chunk on d's stream bracketed by timing events.
 int launch_chunk(Device& d, Mode mode, const LaunchArgs& a, int ring, uint64_t* out) {
   HIPTRY(hipEventRecord(d.ev_start[ring], d.stream));
-  HIPTRY(launch_task(mode, grid_of(d), d.stream, a, d.st, d.mb_dev, out));
+  if (mode == Mode::kSweep && g_pool_lockstep)  // the lockstep sweep: one 1,024-lane workgroup per CU
+    HIPTRY(launch_task(Mode::kSweepLs, d.cus, d.stream, a, d.st, d.mb_dev, out));
+  else
+    HIPTRY(launch_task(mode, grid_of(d), d.stream, a, d.st, d.mb_dev, out));
   HIPTRY(hipEventRecord(d.ev_stop[ring], d.stream));
   return NPOW_OK;
 }

@@ -14,7 +14,9 @@ constexpr int kBlock = 256;  // lanes per workgroup (4 waves of 64)
 constexpr int kLsWaves = 16;                // lockstep pool kernel: waves per workgroup (4 per SIMD) ...
 constexpr int kLsBlock = kLsWaves * 64;     // ... one workgroup per CU
 
-enum class Mode : int { kSweep = 1, kValues = 2 };  // npow_task_kernel (first-win search: npow_pool_kernel)
+// npow_task_kernel (kSweep, kValues) / npow_sweep_kernel_ls (kSweepLs: one 1,024-lane workgroup
+// per CU); first-win searches: npow_pool_kernel*
+enum class Mode : int { kSweep = 1, kValues = 2, kSweepLs = 3 };
 
 // Kernel arguments, passed by value: the kernarg segment lands in SGPRs, so the
 // root-derived uniforms and the threshold cost no memory traffic per nonce

@@ -256,6 +256,101 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
   if (lane == 0 && done) atomicAdd(&st->done_shard[(blockIdx.x % kDoneShards) * 8], (unsigned long long)done);
 }
 
+// ---- Lockstep sweep (npow_sweep_kernel_ls) -------------------------------------------------
+// npow_task_kernel<kSweep> with the lockstep stream (pool_body_ls): 1,024-lane workgroups, one
+// per CU, so everything that shapes a wave's loop is per workgroup.  The unit of work is a row of
+// 16 consecutive 64-nonce blocks, one per wave (block = row * 16 + wave); workgroups claim runs of
+// rows from the same 8 per-XCD counters (thread 0 claims and LDS broadcasts the claim: two
+// barriers per claim of <= max_claim rows), and the stop words (the device abort word, and the
+// pinned host abort word on one claim in poll_mask + 1) are read with the claim, so a cancel
+// lands within one claim (<= 64 rows, ~0.15 ms).  Blocks past the range's end are masked off.
+__global__ __launch_bounds__(kLsBlock) void npow_sweep_kernel_ls(const LaunchArgs a, DevState* __restrict__ st,
+                                                                HostMailbox* __restrict__ mb,
+                                                                uint64_t* __restrict__ out) {
+  __shared__ uint32_t s_claim[3];  // first row, end row (within the sub-range), stop
+  uint64_t u[NPOW_ASM_N_UNIFORMS];
+#pragma unroll
+  for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) u[i] = a.u[i];
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = blockIdx.x;
+  const uint32_t slot = a.claim_slot & 1;
+  if (g == 0 && threadIdx.x < kClaimRanges)
+    __hip_atomic_store(&st->claim[((1 - slot) * kClaimRanges + threadIdx.x) * 8], 0ull, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t T = (uint32_t)((a.count + 63) >> 6);                          // 64-nonce blocks
+  const uint32_t last_lanes = (uint32_t)(a.count - ((uint64_t)(T - 1) << 6));  // 1..64 in block T-1
+  const uint32_t R = (T + kLsWaves - 1) / kLsWaves;                            // rows
+  const uint64_t W2 = 2ull * gridDim.x / kClaimRanges;                         // 2 x workgroups per sub-range
+  const uint64_t lane_nonce = a.base + lane;                                   // + block * 64
+  const uint32_t home = g % kClaimRanges;
+  uint64_t done = 0;
+  uint32_t claims = 0;
+  bool go = true;
+  for (uint32_t k = 0; k < kClaimRanges && go; ++k) {
+    const uint32_t x = (home + k) % kClaimRanges;
+    const uint32_t lo = (uint32_t)((uint64_t)R * x / kClaimRanges);
+    const uint32_t Rx = (uint32_t)((uint64_t)R * (x + 1) / kClaimRanges) - lo;
+    unsigned long long* ctr = &st->claim[(slot * kClaimRanges + x) * 8];
+    uint64_t seen = 0;  // thread 0: the counter as last seen (helping: read before the first claim)
+    if (k && threadIdx.x == 0) seen = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      if (threadIdx.x == 0) {
+        uint32_t c = Rx, end = Rx;
+        if (seen < Rx) {
+          uint64_t n = (Rx - seen) / W2;
+          n = n < 1 ? 1 : (n > a.max_claim ? a.max_claim : n);
+          const uint64_t c64 = atomicAdd(ctr, (unsigned long long)n);
+          seen = c64 + n;
+          if (c64 < Rx) {
+            c = (uint32_t)c64;
+            end = (uint32_t)(seen < Rx ? seen : Rx);
+          }
+        }
+        uint32_t stop = __hip_atomic_load(&st->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (((claims + g) & a.poll_mask) == 0 &&
+            __hip_atomic_load(&mb->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) {
+          __hip_atomic_store(&st->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          stop = 1;
+        }
+        s_claim[0] = c;
+        s_claim[1] = end;
+        s_claim[2] = stop;
+      }
+      ++claims;
+      __syncthreads();
+      const uint32_t c = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_claim[0]);
+      const uint32_t end = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_claim[1]);
+      const uint32_t stop = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_claim[2]);
+      __syncthreads();  // thread 0 rewrites s_claim only after every wave has read it
+      if (stop) {
+        go = false;
+        break;
+      }
+      if (c >= Rx) break;
+      for (uint32_t row = lo + c; row < lo + end; ++row) {
+        const uint32_t b = row * kLsWaves + wv;
+        const uint64_t nonce = lane_nonce + ((uint64_t)b << 6);
+        const uint64_t value = npow_asm_work_value_lockstep(nonce, u);
+        uint64_t hits = __ballot(value >= a.threshold);
+        if (__builtin_expect(b >= T - 1, 0)) {  // the last block may be partial; blocks past it are empty
+          const uint32_t nl = b == T - 1 ? last_lanes : 0u;
+          hits &= nl == 64 ? ~0ull : (1ull << nl) - 1;
+          done += nl;
+        } else {
+          done += 64;
+        }
+        if (__builtin_expect(hits != 0, 0) && ((hits >> lane) & 1)) {  // append every hit
+          const uint32_t hs = atomicAdd(&st->n_hits, 1u);
+          if (hs < a.cap) out[hs] = nonce;
+        }
+      }
+    }
+  }
+  if (lane == 0 && done)
+    atomicAdd(&st->done_shard[((g * kLsWaves + wv) % kDoneShards) * 8], (unsigned long long)done);
+}
+
 // ---- Work pool: many roots per launch ------------------------------------------------------
 // One launch searches every live entry of the device's table (up to kMaxSlots jobs: the
 // DPoW burst, many work_generate requests in flight).  Wave w starts on entry w % n with
@@ -510,9 +605,11 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
   bool end = false;
   for (;;) {
     uint32_t done = 0;
-    uint32_t* const req_word = &s_stop[seg % 3];
+    const uint32_t sw = seg % 3;
     while (it < c.it_end) {
-      const uint32_t verdict = *(volatile uint32_t*)req_word;  // consumed after the hash
+      // an LDS load, consumed after the hash (a volatile or generic-pointer read here compiled to a
+      // flat load waited on before the hash)
+      const uint32_t verdict = __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const uint64_t dead = load_dead(st, c.slot);
       const bool poll = ((it + w) & poll_mask) == 0;
       uint64_t kill, yld;
@@ -534,8 +631,8 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
       } else {
         done += 64;
       }
-      uint32_t req = 0;  // 1: leave the entry, 2: end the launch
       const uint64_t hits = __ballot(hit);
+      bool leave = hits != 0;  // wave-uniform (scalar): leave the entry
       if (__builtin_expect(hits != 0, 0)) {
         const int wl = __builtin_ctzll(hits);
         const uint64_t wn = readlane64(nonce, wl), wval = readlane64(value, wl);
@@ -547,31 +644,33 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
             __hip_atomic_store(&pw->gen, c.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
           }
         }
-        req = 1;
       }
       if (__builtin_expect(poll, 0)) {
         if (readlane64(yld, 0) != yield_base) {  // new jobs wait: end every unbounded entry (pool_body)
           if (lane == 0)
             for (uint32_t k = 0; k < n; ++k)
               if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
-          if (!c.bounded) req = 1;
+          leave = leave || !c.bounded;
         }
         if (readlane64(kill, 0) == c.gen) {
           if (lane == 0) atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen);  // relay
-          req = 1;
+          leave = true;
         }
       }
-      if (readlane64(dead, 0) == c.gen) req = 1;
-      if (budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget) req = 2;
-      if (__builtin_expect(req != 0, 0)) {
-        if (lane == 0) atomicMin(req_word, (it << 1) | (req == 1 ? 1u : 0u));
+      leave = leave || readlane64(dead, 0) == c.gen;
+      const bool late = budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget;  // end the launch
+      if (__builtin_expect(leave || late, 0)) {
+        if (lane == 0)
+          __hip_atomic_fetch_min(&s_stop[sw], (it << 1) | (late ? 0u : 1u), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
         lds_drain();  // complete before the next hash's first barrier
       }
       // the word as read before this hash: requests with value < it0 were filed at the end of
       // iteration it0 - 2 or earlier, behind the previous hash's barriers, so every wave saw
       // them (a later one, value it0, some waves may have seen: all ignore it) -- one verdict
-      if ((__builtin_amdgcn_readfirstlane(verdict) >> 1) < it0) {
-        end = (__builtin_amdgcn_readfirstlane(verdict) & 1) == 0;
+      const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(verdict);
+      if ((v >> 1) < it0) {
+        end = (v & 1) == 0;
         break;
       }
     }
@@ -596,7 +695,8 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
       }
     }
     __syncthreads();
-    const uint32_t next = __builtin_amdgcn_readfirstlane(*(volatile uint32_t*)&s_next);
+    const uint32_t next =
+        __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     if (next == n) break;
     e = next;
     ++seg;
@@ -729,6 +829,9 @@ hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs
   switch (mode) {
     case Mode::kSweep:
       npow_task_kernel<Mode::kSweep><<<grid, kBlock, 0, stream>>>(a, st, mb, out);
+      break;
+    case Mode::kSweepLs:
+      npow_sweep_kernel_ls<<<grid, kLsBlock, 0, stream>>>(a, st, mb, out);
       break;
     case Mode::kValues:
       npow_task_kernel<Mode::kValues><<<grid, kBlock, 0, stream>>>(a, st, mb, out);

@@ -1227,8 +1227,9 @@ def main() -> int:
     ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
     ap.add_argument("--fuse-out", choices=["bitop3", "none"], default="bitop3",
                     help="fold the output xors H0 ^ (v0 ^ v8) into v_bitop3_b32 (fuse_output_xor)")
-    ap.add_argument("--pad", choices=["odd", "even", "none"], default="odd",
-                    help="placement of the stream: 4 (mod 8) [odd], 0 (mod 8) [even], or as it falls")
+    ap.add_argument("--pad", choices=["odd", "even", "none", "odd64", "even64", "odd128", "even128"], default="odd",
+                    help="placement of the stream: 4 (mod 8) [odd], 0 (mod 8) [even], or as it falls; "
+                         "odd64 / even64 / odd128 / even128: 4 or 0 bytes past a 64- or 128-byte boundary")
     args = ap.parse_args()
     global ROTL1_VIA_ADD, VOP3_SIMPLE, SWAP_MOV, PAD, ADD_CC, ROTL1_CC
     ADD_CC = args.add == "cc"
@@ -1240,7 +1241,9 @@ def main() -> int:
                "both": lambda n, h: True, "r16": lambda n, h: n == 16, "r24": lambda n, h: n == 24,
                "r16lo": lambda n, h: n == 16 and h == 0, "r24lo": lambda n, h: n == 24 and h == 0}[args.rotmad]
     SWAP_MOV = args.swapmov
-    PAD = {"odd": ['.p2align 3', 's_nop 0'], "even": ['.p2align 3'], "none": []}[args.pad]
+    PAD = {"odd": ['.p2align 3', 's_nop 0'], "even": ['.p2align 3'], "none": [],
+           "odd64": ['.p2align 6', 's_nop 0'], "even64": ['.p2align 6'],
+           "odd128": ['.p2align 7', 's_nop 0'], "even128": ['.p2align 7']}[args.pad]
     ROTL1_VIA_ADD = args.rotl1 == "add"
     ROTL1_CC = args.rotl1 == "cc"
     VOP3_SIMPLE = args.enc == "vop3"
