@@ -470,7 +470,7 @@ class SclkSampler:
                           f"{int(self.period * 1e3)} ms over the warmup and timed searches"}
 
 
-def _pmc_traffic(name="r02_pmc_pool.json"):
+def _pmc_traffic(name="r02_lockstep_pmc_pool.json" if POOL_KERNEL == "lockstep" else "r02_pmc_pool.json"):
     """HBM bytes per launch of the workload's dominant kernel measured by rocprofv3 PMC passes
     (tools/pmc_bench.sh on that workload; FETCH_SIZE doubled per the gfx950 correction).  PMC
     needs the profiler around the process, so the bench reports the committed measurement;
@@ -525,7 +525,8 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
             "frac": round(achieved / PEAK_TOPS, 4),
             "traffic": _pmc_traffic(),
             "traffic_unit": "HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
-                            "(profiles/r02_pmc_pool.json, tools/pmc_bench.sh); algorithmic bytes: 0",
+                            f"(profiles/{'r02_lockstep_pmc_pool.json' if POOL_KERNEL == 'lockstep' else 'r02_pmc_pool.json'}, "
+                            "tools/pmc_bench.sh); algorithmic bytes: 0",
             "ops_per_nonce": OPS_PER_NONCE,
             "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
             "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
@@ -616,10 +617,12 @@ def workload_sweep(eng, args, rank, world, dist):
         hits = sorted(h for g in gathered for h in g)
     want = [int(h, 16) for h in fx["hits"] if int(h, 16) < count]
     line = result_line(world, 1, 0, nonces, wall, [wall], kms, kn, nl)
-    line["roofline"]["kernel"] = "npow_task_kernel<Mode::kSweep>"
-    line["roofline"]["traffic"] = _pmc_traffic("r01_pmc_sweep.json")
+    ls = POOL_KERNEL == "lockstep"
+    pmc = "r02_lockstep_pmc_sweep.json" if ls else "r01_pmc_sweep.json"
+    line["roofline"]["kernel"] = "npow_sweep_kernel_ls" if ls else "npow_task_kernel<Mode::kSweep>"
+    line["roofline"]["traffic"] = _pmc_traffic(pmc)
     line["roofline"]["traffic_unit"] = ("HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
-                                        "(profiles/r01_pmc_sweep.json, tools/pmc_bench.sh); algorithmic bytes: "
+                                        f"(profiles/{pmc}, tools/pmc_bench.sh); algorithmic bytes: "
                                         "8 per hit")
     line["config"] = {"workload": f"BASELINE configs[2]: exhaustive sweep of [0, 2^{args.sweep_bits}) for the "
                                   "fixture root at fffffff800000000, ranks split the range",

@@ -18,6 +18,10 @@
 //    rotr63 is `v_lshrrev_b32` + `v_lshl_add_u64 x, 1, {hi >> 31, 0}`.
 //  * The hit test is a wave ballot, so a wave leaves the fast path only when one of
 //    its 64 lanes wins.
+//  * Lockstep kernels (default; npow_pool_kernel_ls*, npow_sweep_kernel_ls): the same hash
+//    as npow_hash_asm_lockstep.inc, scheduled in barrier-separated intervals, run by one
+//    1,024-lane workgroup per CU whose waves stay in the same phase;
+//    every loop decision is a workgroup decision.  The kernels below are their seq forms.
 //  * First-win search (npow_pool_kernel): every live job of the device's work
 //    pool in one launch; first win per job by atomicMax on its slot's dead word,
 //    published to a host-coherent mailbox with system-scope stores; every wave
