@@ -105,3 +105,16 @@ def test_sweep_2p36_prefix_pinned_by_hashlib_2p30():
     vals = {n: oracle.work_value_hashlib(root, n) for n in hits30}
     assert all(v >= low for v in vals.values())
     assert [n for n in hits30 if vals[n] >= send] == [int(h, 16) for h in g36["hits"] if int(h, 16) < 1 << 30]
+
+
+def test_sweep_2p36_fixture_pinned_by_hashlib_in_full():
+    """The whole 2^36 fixture equals a hashlib-only exhaustive scan of [0, 2^36)
+    (tests/golden/gen_hashlib_2p36.py: the reference's own CPU path, 6 processes, 3.2 h in the
+    build container): the C oracle that made sweep_2p36.json is pinned on every nonce of the range,
+    not only on its hits."""
+    g36 = load_golden("sweep_2p36.json")
+    gh = load_golden("sweep_2p36_hashlib.json")
+    assert gh["generator"] == "tests/golden/gen_hashlib_2p36.py" and gh["method"].startswith("hashlib.blake2b")
+    for k in ("root", "threshold", "start", "count"):
+        assert gh[k] == g36[k], k
+    assert gh["hits"] == g36["hits"]
