@@ -50,6 +50,7 @@ def body(r, barrier, hkind="align", total=128):
 
 
 WAVES_PER_SIMD = int(os.environ.get("LOCKSTEP_WAVES", "4"))
+GROUPS = int(os.environ.get("LOCKSTEP_GROUPS", "1"))  # workgroups per CU (2: two lockstep groups per SIMD)
 
 
 def main():
@@ -102,40 +103,58 @@ __global__ __launch_bounds__({256 * WAVES_PER_SIMD}) void k{k}(unsigned long lon
     asm volatile("{asm}" ::: {clob});
   __syncthreads();  // the workgroup's last wave, not wave 0 (issue favours the oldest wave)
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
-  if (threadIdx.x == 0) atomicAdd(&out[0], t1 - t0);
+  if (threadIdx.x == 0) {{  // per workgroup: span and where it ran (HW_ID cu/sh/se fields, XCC_ID)
+    out[blockIdx.x * 4 + 0] = t0;
+    out[blockIdx.x * 4 + 1] = t1;
+    out[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_getreg(4 | (31 << 11)) & 0x7f00u;  // cu_id, sh_id, se_id
+    out[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+  }}
 }}''')
         runs.append(f'  run(k{k}, "{name}", {n_ins}, cus, d);')
     src = f'''// GENERATED by tools/experiments/phase_lockstep.py
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
+#include <map>
+#include <vector>
 #define CHECK(x) do {{ hipError_t e = (x); if (e != hipSuccess) {{ fprintf(stderr, "%s\\n", hipGetErrorString(e)); exit(1); }} }} while (0)
 {"".join(kernels)}
 template <class K>
 static void run(K kern, const char* name, int n_ins, int cus, unsigned long long* d) {{
-  kern<<<cus, {256 * WAVES_PER_SIMD}>>>(d);
+  const int G = cus * {GROUPS};
+  kern<<<G, {256 * WAVES_PER_SIMD}>>>(d);
   CHECK(hipDeviceSynchronize());
-  CHECK(hipMemset(d, 0, 8));
-  kern<<<cus, {256 * WAVES_PER_SIMD}>>>(d);
+  kern<<<G, {256 * WAVES_PER_SIMD}>>>(d);
   CHECK(hipDeviceSynchronize());
-  unsigned long long cyc; CHECK(hipMemcpy(&cyc, d, 8, hipMemcpyDeviceToHost));
-  const double per_wg = (double)cyc / cus;                        // cycles of the loop, one workgroup
-  const double ins_per_simd = {WAVES_PER_SIMD}.0 * n_ins * {ITERS};  // waves per SIMD
-  printf("{{\\"variant\\": \\"%s\\", \\"ins_per_block\\": %d, \\"cycles_per_ins\\": %.3f}}\\n", name, n_ins,
-         per_wg / ins_per_simd);
+  std::vector<unsigned long long> h(4 * (size_t)G);
+  CHECK(hipMemcpy(h.data(), d, h.size() * 8, hipMemcpyDeviceToHost));
+  // per CU (s_memtime is one counter per XCD): span from its first start to its last end, over
+  // the instructions every SIMD of that CU issued = its workgroups x waves per SIMD x stream
+  std::map<std::pair<unsigned long long, unsigned long long>, std::vector<int>> cu;
+  for (int g = 0; g < G; ++g) cu[{{h[4 * g + 3], h[4 * g + 2]}}].push_back(g);
+  double sum = 0; int n_cu = 0, most = 0;
+  for (auto& kv : cu) {{
+    unsigned long long lo = ~0ull, hi = 0;
+    for (int g : kv.second) {{ lo = std::min(lo, h[4 * g]); hi = std::max(hi, h[4 * g + 1]); }}
+    sum += (double)(hi - lo) / ((double)kv.second.size() * {WAVES_PER_SIMD} * n_ins * {ITERS});
+    ++n_cu; most = std::max(most, (int)kv.second.size());
+  }}
+  printf("{{\\"variant\\": \\"%s\\", \\"ins_per_block\\": %d, \\"cycles_per_ins\\": %.3f, \\"cus\\": %d, \\"max_groups_per_cu\\": %d}}\\n",
+         name, n_ins, sum / n_cu, n_cu, most);
 }}
 int main() {{
   hipDeviceProp_t p; CHECK(hipGetDeviceProperties(&p, 0));
   const int cus = p.multiProcessorCount;
-  unsigned long long* d; CHECK(hipMalloc(&d, 64));
+  unsigned long long* d; CHECK(hipMalloc(&d, 4 * 8 * (size_t)cus * {GROUPS}));
 {chr(10).join(runs)}
   return 0;
 }}
 '''
-    path = os.path.join(ROOT, "build", f"phase_lockstep_w{WAVES_PER_SIMD}.hip")
+    path = os.path.join(ROOT, "build", f"phase_lockstep_w{WAVES_PER_SIMD}g{GROUPS}.hip")
     os.makedirs(os.path.dirname(path), exist_ok=True)
     open(path, "w").write(src)
-    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-o", os.path.join(ROOT, "build", f"phase_lockstep_w{WAVES_PER_SIMD}"),
+    subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-o", os.path.join(ROOT, "build", f"phase_lockstep_w{WAVES_PER_SIMD}g{GROUPS}"),
                     path], check=True)
 
 
