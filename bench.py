@@ -83,21 +83,35 @@ sys.path.insert(0, os.path.join(HERE, "nano-dpow_amd"))
 SEND = 0xfffffff800000000
 OPS_PER_NONCE = 2232                # int32 VALU ops of one 12-round compression
 PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # MI355X: 256 CU x (4 SIMD x 32 lanes) x 2.4 GHz = 78.6 Tops/s
-# The instruction stream's own issue bound (informational, next to the roofline), per search kernel:
-#  * lockstep (default): the barrier-interval stream with VOP2 xors and shifts, 1,677 VALU
-#    instructions, 5,044 SIMD cycles per wave (64 nonces) with one 1,024-lane workgroup per CU and
-#    no launch tail (tools/experiments/stream_lockstep.py, profiles/r02_lockstep_stream_variants.jsonl
-#    "vop2"), 3.008 cycles each;
+# The generated stream's cost in a tail-free harness (informational, next to the roofline), per
+# search kernel (NANOPOW_POOL_KERNEL / NANOPOW_LS_GROUPS select the kernel at npow_init):
+#  * lockstep2 (default): two 1,024-lane workgroups per CU, the stream loading its own uniforms
+#    (1,677 VALU instructions): 4,852 SIMD cycles per wave-hash (64 nonces) in
+#    tools/experiments/stream_lockstep.py (profiles/r02_stream_bound_g2.jsonl "vop2_ld");
+#  * lockstep (NANOPOW_LS_GROUPS=1): one workgroup per CU, 5,042 cycles (r02_stream_bound_g1.jsonl);
 #  * seq (NANOPOW_POOL_KERNEL=seq): 1,671 instructions at 5,725 cycles, time-budgeted, every SIMD
 #    saturated (tools/valu_mix2.py "real hash stream": profiles/r01_valu_mix2_final_stream.jsonl).
-POOL_KERNEL = "seq" if os.environ.get("NANOPOW_POOL_KERNEL") == "seq" else "lockstep"
-STREAM = {"lockstep": {"cycles": 5044, "valu": 1677, "kernel": "npow_pool_kernel_ls_arg<false>",
-                       "src": "tools/experiments/stream_lockstep.py, profiles/r02_lockstep_stream_variants.jsonl"},
+# The harness is not a strict bound: its workgroups start together and stay in step, while a
+# kernel's two groups per CU drift apart and overlap better (the kernel's own cycles per hash, from
+# its in-kernel clock, are reported beside it).
+POOL_KERNEL = ("seq" if os.environ.get("NANOPOW_POOL_KERNEL") == "seq" else
+               "lockstep" if os.environ.get("NANOPOW_LS_GROUPS") == "1" else "lockstep2")
+STREAM = {"lockstep2": {"cycles": 4852, "valu": 1677, "kernel": "npow_pool_kernel_ls2_arg<false>",
+                        "sweep_kernel": "npow_sweep_kernel_ls2",
+                        "src": "tools/experiments/stream_lockstep.py, profiles/r02_stream_bound_g2.jsonl"},
+          "lockstep": {"cycles": 5042, "valu": 1677, "kernel": "npow_pool_kernel_ls_arg<false>",
+                       "sweep_kernel": "npow_sweep_kernel_ls",
+                       "src": "tools/experiments/stream_lockstep.py, profiles/r02_stream_bound_g1.jsonl"},
           "seq": {"cycles": 5725, "valu": 1671, "kernel": "npow_pool_kernel_arg<false>",
+                  "sweep_kernel": "npow_task_kernel<Mode::kSweep>",
                   "src": "tools/valu_mix2.py, profiles/r01_valu_mix2_final_stream.jsonl"}}[POOL_KERNEL]
 STREAM_CYCLES_PER_HASH = STREAM["cycles"]
 STREAM_CLOCK_GHZ = 2.39   # in-kernel s_memtime / s_memrealtime under this load
 STREAM_BOUND_GNPS = 1024 * 64 * STREAM_CLOCK_GHZ / STREAM_CYCLES_PER_HASH  # 1,024 SIMDs
+PMC_POOL = {"lockstep2": "r02_ls2_pmc_pool.json", "lockstep": "r02_lockstep_pmc_pool.json",
+            "seq": "r02_pmc_pool.json"}[POOL_KERNEL]
+PMC_SWEEP = {"lockstep2": "r02_ls2_pmc_sweep.json", "lockstep": "r02_lockstep_pmc_sweep.json",
+             "seq": "r01_pmc_sweep.json"}[POOL_KERNEL]
 METRIC = "Gnonce/s blake2b-64 per GPU & 8-GPU node; p50 time-to-work at fffffff8"
 
 
@@ -470,7 +484,7 @@ class SclkSampler:
                           f"{int(self.period * 1e3)} ms over the warmup and timed searches"}
 
 
-def _pmc_traffic(name="r02_lockstep_pmc_pool.json" if POOL_KERNEL == "lockstep" else "r02_pmc_pool.json"):
+def _pmc_traffic(name=PMC_POOL):
     """HBM bytes per launch of the workload's dominant kernel measured by rocprofv3 PMC passes
     (tools/pmc_bench.sh on that workload; FETCH_SIZE doubled per the gfx950 correction).  PMC
     needs the profiler around the process, so the bench reports the committed measurement;
@@ -525,21 +539,21 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
             "frac": round(achieved / PEAK_TOPS, 4),
             "traffic": _pmc_traffic(),
             "traffic_unit": "HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
-                            f"(profiles/{'r02_lockstep_pmc_pool.json' if POOL_KERNEL == 'lockstep' else 'r02_pmc_pool.json'}, "
+                            f"(profiles/{PMC_POOL}, "
                             "tools/pmc_bench.sh); algorithmic bytes: 0",
             "ops_per_nonce": OPS_PER_NONCE,
             "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
             "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
             "launches": launches,
-            "issue_bound": {
+            "stream_harness": {
                 "gnps": round(STREAM_BOUND_GNPS, 3),
-                "kernel_frac": (round(kern_nonces / (kern_ms * 1e-3) / 1e9 / STREAM_BOUND_GNPS, 4)
-                                if kern_ms > 0 else None),
-                "what": f"measured issue bound of the {POOL_KERNEL} kernel's generated {STREAM['valu']:,}-"
-                        f"instruction stream ({STREAM_CYCLES_PER_HASH:,} SIMD cycles per 64 nonces at "
-                        f"{STREAM_CLOCK_GHZ} GHz, no launch tail; {STREAM['src']}): the roofline frac is "
-                        "capped by the stream's half-rate share (v_lshl_add_u64, v_alignbit_b32), not by "
-                        "the kernel around it",
+                "cycles_per_hash": STREAM_CYCLES_PER_HASH,
+                "kernel_cycles_per_hash": None,  # filled in once the in-kernel clock is known (main)
+                "what": f"the {POOL_KERNEL} kernel's generated {STREAM['valu']:,}-instruction stream in a tail-free "
+                        f"harness ({STREAM_CYCLES_PER_HASH:,} SIMD cycles per 64 nonces, i.e. {STREAM_BOUND_GNPS:.2f} "
+                        f"Gnonce/s at {STREAM_CLOCK_GHZ} GHz; {STREAM['src']}); kernel_cycles_per_hash is the "
+                        "kernel's own figure at its in-kernel clock; the roofline frac is capped by the stream's "
+                        "half-rate share (v_lshl_add_u64, v_alignbit_b32), not by the kernel around it",
             },
         },
         "cpu_baseline": None,
@@ -617,9 +631,8 @@ def workload_sweep(eng, args, rank, world, dist):
         hits = sorted(h for g in gathered for h in g)
     want = [int(h, 16) for h in fx["hits"] if int(h, 16) < count]
     line = result_line(world, 1, 0, nonces, wall, [wall], kms, kn, nl)
-    ls = POOL_KERNEL == "lockstep"
-    pmc = "r02_lockstep_pmc_sweep.json" if ls else "r01_pmc_sweep.json"
-    line["roofline"]["kernel"] = "npow_sweep_kernel_ls" if ls else "npow_task_kernel<Mode::kSweep>"
+    pmc = PMC_SWEEP
+    line["roofline"]["kernel"] = STREAM["sweep_kernel"]
     line["roofline"]["traffic"] = _pmc_traffic(pmc)
     line["roofline"]["traffic_unit"] = ("HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                                         f"(profiles/{pmc}, tools/pmc_bench.sh); algorithmic bytes: "
@@ -1129,6 +1142,9 @@ def main() -> int:
                                           "timed search launch (libnanopow stats clock_mhz), mean over ranks"}
             line["roofline"]["frac_at_measured_sclk"] = round(line["roofline"]["achieved"] /
                                                               (256 * 128 * mhz * 1e6 / 1e12), 4)
+            kg = line["roofline"]["kernel_gnps"]
+            if kg:  # SIMD cycles per 64-nonce wave-hash at the in-kernel clock (1,024 SIMDs)
+                line["roofline"]["stream_harness"]["kernel_cycles_per_hash"] = round(1024 * 64 * mhz * 1e6 / (kg * 1e9), 1)
         clk = sclk.summary()
         if clk:
             line["sysfs_sclk_mhz"] = clk

@@ -76,6 +76,7 @@ std::atomic<uint32_t> g_pool_blocks_per_cu{4};
 // once, before the first launch (npow_init).
 bool g_pool_lockstep = true;
 uint32_t g_ls_lds = 0;
+int g_ls_groups = 2;  // NANOPOW_LS_GROUPS=1: one 1,024-lane workgroup per CU (npow_pool_kernel_ls*)
 
 std::vector<Device*> select_devices(uint64_t mask) {
   std::vector<Device*> out;
@@ -109,8 +110,9 @@ struct Inflight {
 // Launch one chunk on d's stream bracketed by timing events.
 int launch_chunk(Device& d, Mode mode, const LaunchArgs& a, int ring, uint64_t* out) {
   HIPTRY(hipEventRecord(d.ev_start[ring], d.stream));
-  if (mode == Mode::kSweep && g_pool_lockstep)  // the lockstep sweep: one 1,024-lane workgroup per CU
-    HIPTRY(launch_task(Mode::kSweepLs, d.cus, d.stream, a, d.st, d.mb_dev, out));
+  if (mode == Mode::kSweep && g_pool_lockstep)  // the lockstep sweep: 1,024-lane workgroups, 1 or 2 per CU
+    HIPTRY(launch_task(g_ls_groups == 2 ? Mode::kSweepLs2 : Mode::kSweepLs, d.cus * g_ls_groups, d.stream, a, d.st,
+                       d.mb_dev, out));
   else
     HIPTRY(launch_task(mode, grid_of(d), d.stream, a, d.st, d.mb_dev, out));
   HIPTRY(hipEventRecord(d.ev_stop[ring], d.stream));
@@ -314,6 +316,7 @@ int npow_init(int* n_devices) try {
   // the multi-device first-win path runs on a one-GPU machine.
   if (const char* k = getenv("NANOPOW_POOL_KERNEL")) g_pool_lockstep = strcmp(k, "seq") != 0;
   if (const char* l = getenv("NANOPOW_LS_LDS")) g_ls_lds = (uint32_t)atoi(l);
+  if (const char* k = getenv("NANOPOW_LS_GROUPS")) g_ls_groups = atoi(k) == 1 ? 1 : 2;
   int n_logical = n;
   if (const char* v = getenv("NANOPOW_VIRTUAL_DEVICES")) {
     const int k = atoi(v);

@@ -78,10 +78,11 @@ inline int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load()
 // Search launches: the lockstep kernel (default) with one 1,024-lane workgroup per CU, or the
 // seq kernel with g_pool_blocks_per_cu 256-lane workgroups per CU (NANOPOW_POOL_KERNEL=seq).
 extern bool g_pool_lockstep;
-extern uint32_t g_ls_lds;  // lockstep: dynamic LDS bytes per workgroup (NANOPOW_LS_LDS)
+extern uint32_t g_ls_lds;     // lockstep: dynamic LDS bytes per workgroup (NANOPOW_LS_LDS)
+extern int g_ls_groups;       // lockstep: workgroups per CU, 1 or 2 (NANOPOW_LS_GROUPS)
 inline PoolShape pool_shape(const Device& d) {
-  if (g_pool_lockstep) return PoolShape{true, d.cus, g_ls_lds};
-  return PoolShape{false, d.cus * (int)g_pool_blocks_per_cu.load(), 0};
+  if (g_pool_lockstep) return PoolShape{true, d.cus * g_ls_groups, g_ls_lds, g_ls_groups};
+  return PoolShape{false, d.cus * (int)g_pool_blocks_per_cu.load(), 0, 1};
 }
 inline uint32_t poll_mask() {
   uint32_t p = g_poll.load();

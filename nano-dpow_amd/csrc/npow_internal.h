@@ -7,6 +7,7 @@
 #include "npow_blake2b.h"
 #include "npow_hash_asm.inc"
 #include "npow_hash_asm_lockstep.inc"
+#include "npow_hash_asm_lockstep_ld.inc"
 
 namespace npow {
 
@@ -16,7 +17,7 @@ constexpr int kLsBlock = kLsWaves * 64;     // ... one workgroup per CU
 
 // npow_task_kernel (kSweep, kValues) / npow_sweep_kernel_ls (kSweepLs: one 1,024-lane workgroup
 // per CU); first-win searches: npow_pool_kernel*
-enum class Mode : int { kSweep = 1, kValues = 2, kSweepLs = 3 };
+enum class Mode : int { kSweep = 1, kValues = 2, kSweepLs = 3, kSweepLs2 = 4 };  // Ls2: two workgroups per CU
 
 // Kernel arguments, passed by value: the kernarg segment lands in SGPRs, so the
 // root-derived uniforms and the threshold cost no memory traffic per nonce
@@ -170,6 +171,7 @@ struct PoolShape {
   bool lockstep;  // npow_pool_kernel_ls* (1,024-lane workgroups) instead of npow_pool_kernel*
   int grid;       // workgroups
   uint32_t lds;   // lockstep: dynamic LDS bytes per workgroup (> half a CU's keeps one per CU)
+  int groups;     // lockstep: workgroups per CU (2: npow_pool_kernel_ls2*, 8 waves per SIMD)
   uint32_t units() const { return lockstep ? (uint32_t)grid : (uint32_t)grid * (kBlock / 64); }
   uint32_t waves_per_unit() const { return lockstep ? (uint32_t)kLsWaves : 1u; }
   // nonces a bounded entry e of n can cover in one launch of `iters` wave iterations
@@ -178,6 +180,11 @@ struct PoolShape {
     return (uint64_t)(U / n + (e < U % n ? 1u : 0u)) * waves_per_unit() * iters * 64;
   }
   uint64_t full(uint32_t iters) const { return (uint64_t)units() * waves_per_unit() * iters * 64; }
+  // The iteration cap of a launch: with two lockstep workgroups per CU a wave iteration takes
+  // twice as long, so half the cap keeps a launch's longest duration (and its nonce span) unchanged.
+  uint32_t launch_iters(uint32_t iters) const {
+    return lockstep && groups == 2 ? (iters > 1 ? iters / 2 : 1u) : iters;
+  }
 };
 
 // Launchers (defined in npow_kernel.hip).

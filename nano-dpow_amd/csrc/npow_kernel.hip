@@ -268,13 +268,18 @@ __global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, D
 // barriers per claim of <= max_claim rows), and the stop words (the device abort word, and the
 // pinned host abort word on one claim in poll_mask + 1) are read with the claim, so a cancel
 // lands within one claim (<= 64 rows, ~0.15 ms).  Blocks past the range's end are masked off.
-__global__ __launch_bounds__(kLsBlock) void npow_sweep_kernel_ls(const LaunchArgs a, DevState* __restrict__ st,
-                                                                HostMailbox* __restrict__ mb,
-                                                                uint64_t* __restrict__ out) {
+template <bool LD>
+__device__ __forceinline__ void sweep_body_ls(const LaunchArgs& a, DevState* __restrict__ st,
+                                              HostMailbox* __restrict__ mb, uint64_t* __restrict__ out) {
   __shared__ uint32_t s_claim[3];  // first row, end row (within the sub-range), stop
   uint64_t u[NPOW_ASM_N_UNIFORMS];
+  const uint64_t* up = nullptr;  // LD: the uniforms in the kernel arguments, loaded by the stream
+  if constexpr (LD) {
+    up = ((const LaunchArgs*)__builtin_amdgcn_kernarg_segment_ptr())->u;
+  } else {
 #pragma unroll
-  for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) u[i] = a.u[i];
+    for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) u[i] = a.u[i];
+  }
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t g = blockIdx.x;
@@ -335,7 +340,11 @@ __global__ __launch_bounds__(kLsBlock) void npow_sweep_kernel_ls(const LaunchArg
       for (uint32_t row = lo + c; row < lo + end; ++row) {
         const uint32_t b = row * kLsWaves + wv;
         const uint64_t nonce = lane_nonce + ((uint64_t)b << 6);
-        const uint64_t value = npow_asm_work_value_lockstep(nonce, u);
+        uint64_t value;
+        if constexpr (LD)
+          value = npow_asm_work_value_lockstep_ld(nonce, up);
+        else
+          value = npow_asm_work_value_lockstep(nonce, u);
         uint64_t hits = __ballot(value >= a.threshold);
         if (__builtin_expect(b >= T - 1, 0)) {  // the last block may be partial; blocks past it are empty
           const uint32_t nl = b == T - 1 ? last_lanes : 0u;
@@ -355,6 +364,19 @@ __global__ __launch_bounds__(kLsBlock) void npow_sweep_kernel_ls(const LaunchArg
     atomicAdd(&st->done_shard[((g * kLsWaves + wv) % kDoneShards) * 8], (unsigned long long)done);
 }
 
+__global__ __launch_bounds__(kLsBlock) void npow_sweep_kernel_ls(const LaunchArgs a, DevState* __restrict__ st,
+                                                                HostMailbox* __restrict__ mb,
+                                                                uint64_t* __restrict__ out) {
+  sweep_body_ls<false>(a, st, mb, out);
+}
+
+// Two lockstep workgroups per CU: 8 waves per SIMD (64 VGPRs, 80 SGPRs per wave).
+__global__ __launch_bounds__(kLsBlock, 8) void npow_sweep_kernel_ls2(const LaunchArgs a, DevState* __restrict__ st,
+                                                                    HostMailbox* __restrict__ mb,
+                                                                    uint64_t* __restrict__ out) {
+  sweep_body_ls<true>(a, st, mb, out);
+}
+
 // ---- Work pool: many roots per launch ------------------------------------------------------
 // One launch searches every live entry of the device's table (up to kMaxSlots jobs: the
 // DPoW burst, many work_generate requests in flight).  Wave w starts on entry w % n with
@@ -368,6 +390,7 @@ __device__ uint64_t npow_wave_probe[32768 * 4];
 
 struct PoolCursor {
   uint64_t u[NPOW_ASM_N_UNIFORMS];
+  const uint64_t* up;  // the entry's uniforms in memory (lockstep LD kernels: the stream loads them)
   uint64_t threshold, base, gen;
   uint32_t slot;
   uint32_t K, j;      // block index b = it * K + j; nonce = base + b * 64 + lane
@@ -557,10 +580,15 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
 //  * leaving an entry: wave 0 picks the next live unbounded entry and broadcasts it through
 //    LDS (one __syncthreads); each entry segment has its own request word (3 rotate: the word
 //    of segment s + 1 is reset at the end of segment s, after its last reader, segment s - 2).
+template <bool LD>
 __device__ __forceinline__ void pool_load_ls(const PoolEntry* __restrict__ pe, PoolCursor& c, uint32_t g, uint32_t wv,
                                              uint32_t G, uint32_t n, uint32_t e, uint32_t iters) {
+  if constexpr (LD) {
+    c.up = pe->u;
+  } else {
 #pragma unroll
-  for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) c.u[i] = pe->u[i];
+    for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) c.u[i] = pe->u[i];
+  }
   c.threshold = pe->threshold;
   c.base = pe->base;
   c.gen = pe->gen;
@@ -587,7 +615,9 @@ __device__ __forceinline__ void pool_load_ls(const PoolEntry* __restrict__ pe, P
 
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-template <bool BOUNDED>
+// LD: the stream loads the entry's uniforms itself (npow_hash_asm_lockstep_ld.inc), so the kernel
+// fits 8 waves per SIMD -- two lockstep workgroups per CU (npow_pool_kernel_ls2*).
+template <bool BOUNDED, bool LD>
 __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
                                              PoolMailbox* __restrict__ mb, const uint64_t t_start) {
   __shared__ uint32_t s_stop[3];  // per entry segment (mod 3): the earliest stop request
@@ -604,7 +634,7 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
 
   uint32_t e = g % n, seg = 0;
   PoolCursor c;
-  pool_load_ls(&tab->e[e], c, g, wv, G, n, e, iters);
+  pool_load_ls<LD>(&tab->e[e], c, g, wv, G, n, e, iters);
   uint32_t it = 0;
   bool end = false;
   for (;;) {
@@ -625,7 +655,11 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
       const uint32_t it0 = it;
       const uint32_t b = it * c.K + c.j;
       const uint64_t nonce = c.base + ((uint64_t)b << 6) + lane;
-      const uint64_t value = npow_asm_work_value_lockstep(nonce, c.u);
+      uint64_t value;
+      if constexpr (LD)
+        value = npow_asm_work_value_lockstep_ld(nonce, c.up);
+      else
+        value = npow_asm_work_value_lockstep(nonce, c.u);
       ++it;
       bool hit = value >= c.threshold;
       if constexpr (BOUNDED) {
@@ -704,7 +738,139 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
     if (next == n) break;
     e = next;
     ++seg;
-    pool_load_ls(&tab->e[e], c, g, wv, G, n, e, iters);
+    pool_load_ls<LD>(&tab->e[e], c, g, wv, G, n, e, iters);
+  }
+}
+
+// The two-workgroups-per-CU form (npow_pool_kernel_ls2*): the same protocol as pool_body_ls with
+// the register budget of 8 waves per SIMD (64 VGPRs, 80 SGPRs, of which the stream takes 38 for
+// the uniforms it loads itself).  The loop keeps only what every iteration needs in registers:
+// the nonce advances in a VGPR by K * 64, the block index by K; the entry's fields, the table and
+// the mailbox are re-read inside the rare branches (a win, a poll, leaving an entry).
+__device__ __noinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
+                                             uint64_t wn, uint64_t wv) {
+  if (atomicMax(&st->slot[slot].dead, (unsigned long long)gen) < gen) {  // first win
+    PoolWin* pw = &mb->win[slot];
+    __hip_atomic_store(&pw->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&pw->value, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&pw->gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// A polling wave (lane 0 only): the host words of the entry.  Returns true when the wave's
+// workgroup must leave the entry (new jobs wait and the entry is unbounded, or it was killed).
+__device__ __noinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e) {
+  const PoolEntry* pe = &tab->e[e];
+  bool leave = false;
+  if (__hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != tab->yield_base) {
+    for (uint32_t k = 0; k < tab->n; ++k)
+      if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
+    leave = !pe->bounded;
+  }
+  if (__hip_atomic_load(&mb->kill[pe->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == pe->gen) {
+    atomicMax(&st->slot[pe->slot].dead, (unsigned long long)pe->gen);  // relay
+    leave = true;
+  }
+  return leave;
+}
+
+template <bool BOUNDED>
+__device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
+                                              PoolMailbox* __restrict__ mb, const uint64_t t_start) {
+  __shared__ uint32_t s_stop[3];  // per entry segment (mod 3): the earliest stop request (pool_body_ls)
+  __shared__ uint32_t s_flag;     // lane 0 of a polling wave -> its wave: leave the entry
+  __shared__ uint32_t s_next;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t g = blockIdx.x, G = gridDim.x;
+  const uint32_t w = g * kLsWaves + wv;
+  const uint32_t n = tab->n, iters = tab->iters;
+  if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
+  __syncthreads();
+  (void)s_flag;
+
+  uint32_t e = g % n, seg = 0, it = 0;
+  bool end = false;
+  for (;;) {
+    const PoolEntry* pe = &tab->e[e];
+    PoolCursor c;
+    pool_load_ls<true>(pe, c, g, wv, G, n, e, iters);
+    const uint32_t sw = seg % 3;
+    const uint32_t poll_mask = tab->poll_mask, budget = tab->budget;
+    unsigned long long* const dead_p = &st->slot[c.slot].dead;
+    uint32_t b = it * c.K + c.j;
+    uint64_t nonce = c.base + ((uint64_t)b << 6) + lane;
+    const uint64_t step = (uint64_t)c.K << 6;
+    uint32_t done = 0;
+    while (it < c.it_end) {
+      const uint32_t verdict = __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint64_t dead = __hip_atomic_load(dead_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
+      const uint32_t it0 = it;
+      const uint64_t value = npow_asm_work_value_lockstep_ld(nonce, c.up);
+      ++it;
+      bool hit = value >= c.threshold;
+      if constexpr (BOUNDED) {
+        const uint32_t in_lanes = b < c.last_b ? 64u : (b == c.last_b ? c.tail : 0u);
+        hit = hit && lane < in_lanes;
+        done += in_lanes;
+      } else {
+        done += 64;
+      }
+      const uint64_t hits = __ballot(hit);
+      bool leave = hits != 0;
+      if (__builtin_expect(hits != 0, 0)) {
+        const int wl = __builtin_ctzll(hits);
+        const uint64_t wn = readlane64(nonce, wl), wval = readlane64(value, wl);
+        if (lane == 0) ls2_publish_win(st, mb, c.slot, c.gen, wn, wval);
+      }
+      if (__builtin_expect(((it0 + w) & poll_mask) == 0, 0)) {
+        if (lane == 0) s_flag = ls2_poll(tab, st, mb, e) ? 1u : 0u;  // the wave's own LDS word use:
+        lds_drain();                                                 // no other wave touches s_flag
+        leave = leave || __builtin_amdgcn_readfirstlane(
+                             __hip_atomic_load(&s_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) != 0;
+      }
+      leave = leave || readlane64(dead, 0) == c.gen;
+      const bool late = budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget;
+      if (__builtin_expect(leave || late, 0)) {
+        if (lane == 0)
+          __hip_atomic_fetch_min(&s_stop[sw], (it << 1) | (late ? 0u : 1u), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_drain();
+      }
+      nonce += step;
+      b += c.K;
+      const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(verdict);
+      if ((v >> 1) < it0) {  // the uniform verdict (pool_body_ls)
+        end = (v & 1) == 0;
+        break;
+      }
+    }
+    if (lane == 0 && done)
+      atomicAdd(&st->done[c.slot][(w % kPoolDoneShards) * 8], (unsigned long long)done);
+    if (it >= iters || end) break;
+    if (wv == 0) {
+      uint32_t next = n;
+      for (uint32_t k = 1; k < n; ++k) {
+        uint32_t e2 = e + k;
+        if (e2 >= n) e2 -= n;
+        const PoolEntry* p2 = &tab->e[e2];
+        if (p2->bounded) continue;
+        if (load_dead(st, p2->slot) >= p2->gen) continue;
+        next = e2;
+        break;
+      }
+      if (lane == 0) {
+        s_next = next;
+        s_stop[(seg + 1) % 3] = ~0u;
+      }
+    }
+    __syncthreads();
+    const uint32_t next =
+        __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+    if (next == n) break;
+    e = next;
+    ++seg;
   }
 }
 
@@ -759,7 +925,7 @@ void npow_pool_kernel_arg(const PoolTableArg targ, PoolDevState* __restrict__ st
   clk_end(tab, mb, t_start, c_start);
 }
 
-// The lockstep variants: 1,024-lane workgroups, one per CU (pool_body_ls).
+// The lockstep variants: 1,024-lane workgroups, one per CU (pool_body_ls); ls2: two per CU.
 template <bool BOUNDED>
 __global__ __launch_bounds__(kLsBlock) void npow_pool_kernel_ls(const PoolTable* __restrict__ tab,
                                                                PoolDevState* __restrict__ st,
@@ -767,7 +933,7 @@ __global__ __launch_bounds__(kLsBlock) void npow_pool_kernel_ls(const PoolTable*
   uint64_t t_start;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
   const uint64_t c_start = clk_begin();
-  pool_body_ls<BOUNDED>(tab, st, mb, t_start);
+  pool_body_ls<BOUNDED, false>(tab, st, mb, t_start);
   clk_end(tab, mb, t_start, c_start);
 }
 
@@ -780,13 +946,42 @@ __global__ __launch_bounds__(kLsBlock) void npow_pool_kernel_ls_arg(const PoolTa
   (void)targ;
   const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();
   const uint64_t c_start = clk_begin();
-  pool_body_ls<BOUNDED>(tab, st, mb, t_start);
+  pool_body_ls<BOUNDED, false>(tab, st, mb, t_start);
+  clk_end(tab, mb, t_start, c_start);
+}
+
+template <bool BOUNDED>
+__global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2(const PoolTable* __restrict__ tab,
+                                                                   PoolDevState* __restrict__ st,
+                                                                   PoolMailbox* __restrict__ mb) {
+  uint64_t t_start;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
+  const uint64_t c_start = clk_begin();
+  pool_body_ls2<BOUNDED>(tab, st, mb, t_start);
+  clk_end(tab, mb, t_start, c_start);
+}
+
+template <bool BOUNDED>
+__global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2_arg(const PoolTableArg targ,
+                                                                       PoolDevState* __restrict__ st,
+                                                                       PoolMailbox* __restrict__ mb) {
+  uint64_t t_start;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
+  (void)targ;
+  const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();
+  const uint64_t c_start = clk_begin();
+  pool_body_ls2<BOUNDED>(tab, st, mb, t_start);
   clk_end(tab, mb, t_start, c_start);
 }
 
 hipError_t launch_pool(const PoolShape& sh, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
                        PoolMailbox* mb) {
-  if (sh.lockstep) {
+  if (sh.lockstep && sh.groups == 2) {
+    if (bounded)
+      npow_pool_kernel_ls2<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
+    else
+      npow_pool_kernel_ls2<false><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
+  } else if (sh.lockstep) {
     if (bounded)
       npow_pool_kernel_ls<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
     else
@@ -804,7 +999,12 @@ hipError_t launch_pool_arg(const PoolShape& sh, hipStream_t stream, const PoolTa
   if (host_tab.n > (uint32_t)kArgEntries) return hipErrorInvalidValue;
   PoolTableArg a;
   memcpy(&a, &host_tab, pool_table_bytes(host_tab.n));
-  if (sh.lockstep) {
+  if (sh.lockstep && sh.groups == 2) {
+    if (bounded)
+      npow_pool_kernel_ls2_arg<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
+    else
+      npow_pool_kernel_ls2_arg<false><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
+  } else if (sh.lockstep) {
     if (bounded)
       npow_pool_kernel_ls_arg<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
     else
@@ -836,6 +1036,9 @@ hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs
       break;
     case Mode::kSweepLs:
       npow_sweep_kernel_ls<<<grid, kLsBlock, 0, stream>>>(a, st, mb, out);
+      break;
+    case Mode::kSweepLs2:
+      npow_sweep_kernel_ls2<<<grid, kLsBlock, 0, stream>>>(a, st, mb, out);
       break;
     case Mode::kValues:
       npow_task_kernel<Mode::kValues><<<grid, kBlock, 0, stream>>>(a, st, mb, out);

@@ -506,8 +506,8 @@ int Worker::launch() {
       std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - front_start_).count() <
           (double)g_budget_us.load() - kPrelaunchUs)
     return NPOW_OK;
-  const uint32_t iters = g_iters.load();
   const PoolShape sh = pool_shape(d_);
+  const uint32_t iters = sh.launch_iters(g_iters.load());
   PoolTable& t = *d_.h_tab[ring_];
   uint32_t n = 0;
   bool bounded = false;

@@ -23,6 +23,8 @@ ITERS = int(os.environ.get("LOCKSTEP_ITERS", "400"))
 # streams are then bound to v2..v63 (nonce v[6:7], value v4/v5) so the kernel fits 64 VGPRs
 GROUPS = int(os.environ.get("LOCKSTEP_GROUPS", "1"))
 NONCE, VLO, VHI = (6, 4, 5) if GROUPS > 1 else (100, 102, 103)
+# LOCKSTEP_SKEW=P: odd workgroups first issue P dummy xors, so the two groups of a CU start out of phase
+SKEW = int(os.environ.get("LOCKSTEP_SKEW", "0"))
 
 
 def bind(path):
@@ -60,20 +62,34 @@ def main():
         n_bar = sum(1 for ln in lines if ln.startswith("s_barrier"))
         assert all(sum(1 for ln in st if ln.startswith("s_barrier")) == n_bar for st in streams), "barrier counts differ"
         asms = ["\\n\\t".join(st) for st in streams]
-        if len(asms) == 1:
-            body = f'asm volatile("{asms[0]}" ::: {clob}, {sclob});'
+        # a --uload stream reads its uniforms from memory (%[up]: any readable buffer; the values do
+        # not matter) into fixed SGPRs, which it clobbers
+        up = "%[up]" in asms[0]
+        if up:
+            b0 = int(re.search(r"s_load_dwordx16 s\[(\d+):", asms[0]).group(1))
+            sc = ", ".join(f'"s{r}"' for r in range(b0 - 2, b0 + 36))  # gen_hash_asm.uload_layout
+            ops = f': : [up] "s"(out) : {clob}, {sc}'
         else:
-            body = (f'if ((wv >> {bit}) & 1) asm volatile("{asms[1]}" ::: {clob}, {sclob});\n'
-                    f'    else asm volatile("{asms[0]}" ::: {clob}, {sclob});')
+            ops = f'::: {clob}, {sclob}'
+        if len(asms) == 1:
+            body = f'asm volatile("{asms[0]}" {ops});'
+        else:
+            body = (f'if ((wv >> {bit}) & 1) asm volatile("{asms[1]}" {ops});\n'
+                    f'    else asm volatile("{asms[0]}" {ops});')
+        # one __syncthreads per hash for a stream without barriers of its own (its waves would
+        # drift apart); a lockstep stream's 96 barriers already keep them together
+        skew = "\\n\\t".join(["v_xor_b32_e32 v2, v3, v2"] * max(SKEW, 1))
+        sync = "" if n_bar else "__syncthreads();  // one per hash: the seq stream has none of its own"
         kernels.append(f'''
 __global__ __launch_bounds__(1024) void k{k}(unsigned long long* out) {{
   asm volatile("v_mov_b32 v{NONCE}, v0\\n\\tv_mov_b32 v{NONCE + 1}, 0" ::: {clob});
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   __syncthreads();
   const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  if ({SKEW} && (blockIdx.x & 1)) asm volatile("{skew}" ::: "v2", "v3");
   for (int it = 0; it < {ITERS}; ++it) {{
     {body}
-    __syncthreads();  // one per hash: the seq stream has none of its own
+    {sync}
   }}
   const unsigned long long t1 = __builtin_amdgcn_s_memtime();
   if (threadIdx.x == 0) {{  // per workgroup: span and CU (HW_ID cu/sh/se fields, XCC_ID)
@@ -125,10 +141,11 @@ int main() {{
   return 0;
 }}
 '''
-    path = os.path.join(ROOT, "build", f"stream_lockstep_g{GROUPS}.hip")
+    tag = f"g{GROUPS}" + (f"s{SKEW}" if SKEW else "")
+    path = os.path.join(ROOT, "build", f"stream_lockstep_{tag}.hip")
     open(path, "w").write(src)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-o",
-                    os.path.join(ROOT, "build", f"stream_lockstep_g{GROUPS}"), path], check=True)
+                    os.path.join(ROOT, "build", f"stream_lockstep_{tag}"), path], check=True)
 
 
 if __name__ == "__main__":

@@ -982,6 +982,49 @@ def fuse_output_xor(lines: List[str], counts: Dict[str, int]) -> List[str]:
     return out
 
 
+def uload_layout(base: int, nu: int) -> Dict[int, str]:
+    """--uload BASE: SGPR -> the named 32-bit value it holds.  u[i] in s[BASE+2i : BASE+2i+1] (the
+    table's byte layout, so three scalar loads fill them); k8, k16 just below BASE and h0_lo, h0_hi
+    just above the uniforms (BASE = 36: s34..s71, clear of s32 and of the s72+ that an 8-wave
+    kernel reserves)."""
+    out: Dict[int, str] = {}
+    for i in range(nu):
+        out[base + 2 * i] = f"u{i}_lo"
+        out[base + 2 * i + 1] = f"u{i}_hi"
+    top = base + 2 * nu
+    for r, nm in ((base - 2, "k8"), (base - 1, "k16"), (top, "h0_lo"), (top + 1, "h0_hi")):
+        out[r] = nm
+    return out
+
+
+def uload_transform(lines: List[str], base: int, nu: int) -> List[str]:
+    """The stream reading its uniforms from fixed SGPRs that it loads itself from %[up] (the
+    entry's u[] in memory): the compiler then keeps no uniform live across the block, which
+    leaves room for 8 waves per SIMD (80 SGPRs).  Prologue: scalar loads, the constants, a wait."""
+    assert base % 4 == 0 and nu <= 24
+    where = {v: k for k, v in uload_layout(base, nu).items()}
+    out = []
+    for ln in lines:
+        ln = re.sub(r"%\[u(\d+)\]", lambda m: f"s[{base + 2 * int(m.group(1))}:{base + 2 * int(m.group(1)) + 1}]", ln)
+        ln = re.sub(r"%\[(u\d+_lo|u\d+_hi|k8|k16|h0_lo|h0_hi)\]", lambda m: f"s{where[m.group(1)]}", ln)
+        out.append(ln)
+    pro = []
+    off = 0
+    while off < nu:
+        k = min(8, nu - off)
+        width = {8: 16, 4: 8, 2: 4, 1: 2}[k] if k in (8, 4, 2, 1) else None
+        if width is None:  # split an odd remainder
+            k = max(x for x in (8, 4, 2, 1) if x <= k)
+            width = 2 * k
+        r = base + 2 * off
+        pro.append(f"s_load_dwordx{width} s[{r}:{r + width - 1}], %[up], 0x{8 * off:x}")
+        off += k
+    pro += [f"s_movk_i32 s{where['k8']}, 0x100", f"s_mov_b32 s{where['k16']}, 0x10000",
+            f"s_mov_b32 s{where['h0_lo']}, 0x{H0 & M32:08x}", f"s_mov_b32 s{where['h0_hi']}, 0x{H0 >> 32:08x}",
+            "s_waitcnt lgkmcnt(0)"]
+    return pro + out
+
+
 def _pair_regs(tok: str) -> List[str]:
     lo, hi = tok[2:-1].split(":")
     return [f"v{r}" for r in range(int(lo), int(hi) + 1)]
@@ -994,6 +1037,12 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
     for i, u in enumerate(uni_vals):
         named[f"u{i}_lo"] = u & M32
         named[f"u{i}_hi"] = u >> 32
+    # --uload: the uniforms and constants sit in fixed SGPRs (uload_layout), loaded by the block itself
+    sregs: Dict[int, int] = {}
+    base = next((int(m.group(1)) for ln in lines for m in [re.match(r"s_load_dwordx16 s\[(\d+):", ln)] if m), None)
+    if base is not None:
+        for k, v in uload_layout(base, len(uni_vals)).items():
+            sregs[k] = named[v]
 
     def rd32(tok: str) -> int:
         tok = tok.strip()
@@ -1003,6 +1052,8 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
             return named[tok[2:-1]]
         if tok.startswith("v") and tok[1:].isdigit():
             return regs[int(tok[1:])]
+        if tok.startswith("s") and tok[1:].isdigit():
+            return sregs[int(tok[1:])]
         return int(tok)
 
     def rd64(tok: str) -> int:
@@ -1011,6 +1062,9 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
             return nonce
         if tok.startswith("%[u"):
             return uni_vals[int(tok[3:-1])]
+        if tok.startswith("s["):
+            lo = int(tok[2:-1].split(":")[0])
+            return sregs[lo] | (sregs[lo + 1] << 32)
         assert tok.startswith("v["), tok
         lo, hi = tok[2:-1].split(":")
         lo, hi = int(lo), int(hi)
@@ -1026,8 +1080,8 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
 
     carry: Dict[str, int] = {}  # "vcc" or "s[k:k+1]" -> the carry bit it holds
     for ln in lines:
-        if ln.startswith(".") or ln.startswith("s_nop") or ln.startswith("s_barrier"):
-            continue  # placement directives / padding / lockstep interval ends
+        if ln.startswith(".") or ln.startswith("s_"):
+            continue  # placement directives / padding / lockstep interval ends / the --uload prologue
         opc, rest = ln.split(" ", 1)
         opc = opc[:-4] if opc.endswith("_e64") else opc
         ops = [t.strip() for t in rest.split(",")]
@@ -1126,9 +1180,14 @@ def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List
     text = "\n".join(lines)
     if "vcc" in text:
         clobbers += ', "vcc"'
-    for k in sorted({int(m) for m in re.findall(r"s\[(\d+):\d+\]", text)}):
-        clobbers += f', "s{k}", "s{k + 1}"'
-    ops_in = []
+    uload = "%[up]" in text
+    if uload:  # the fixed SGPRs the block loads its uniforms and constants into
+        lo = int(re.search(r"s_load_dwordx16 s\[(\d+):", text).group(1))
+        clobbers += "".join(f', "s{k}"' for k in sorted(uload_layout(lo, nu)))
+    else:
+        for k in sorted({int(m) for m in re.findall(r"s\[(\d+):\d+\]", text)}):
+            clobbers += f', "s{k}", "s{k + 1}"'
+    ops_in = ['[up] "s"(up)'] if uload else []
     for nm, expr in [("nonce", "nonce"), ("nonce_lo", "(uint32_t)nonce"), ("nonce_hi", "(uint32_t)(nonce >> 32)"),
                      ("k8", "256u"), ("k16", "65536u"),
                      ("h0_lo", f"0x{H0 & M32:08x}u"), ("h0_hi", f"0x{H0 >> 32:08x}u")]:
@@ -1142,7 +1201,14 @@ def write_inc(path: str, lines: List[str], frontier: List[Node], host_prog: List
         if f"%[u{i}_hi]" in text:
             ops_in.append(f'[u{i}_hi] "s"((uint32_t)(u[{i}] >> 32))')
     uni_ops = ",\n        ".join(ops_in)
-    body = "\n".join(f'      "{ln}\\n"' for ln in PAD + lines)
+    npro = 0
+    while uload and not lines[npro].startswith("v_"):
+        npro += 1  # the --uload prologue goes before the placement pad: the pad places the VALU stream
+    pad = PAD
+    if uload and lines[npro - 1] == "s_waitcnt lgkmcnt(0)" and PAD[-1:] == ["s_nop 0"]:
+        npro -= 1  # the wait takes the pad's 4-byte s_nop slot: the pad's fill runs while the loads land
+        pad = PAD[:-1]
+    body = "\n".join(f'      "{ln}\\n"' for ln in lines[:npro] + pad + lines[npro:])
     cnt_txt = ", ".join(f"{k} {v}" for k, v in sorted(counts.items()))
     n_bar = sum(1 for ln in lines if ln.startswith("s_barrier"))
     if func == "npow_asm_work_value":
@@ -1162,6 +1228,11 @@ static inline void npow_asm_uniforms(const uint64_t m[4], uint64_t u[NPOW_ASM_N_
 
 static_assert(NPOW_ASM_N_UNIFORMS == {nu}, "include after the primary stream: the same uniforms");
 """
+    if uload:
+        prologue += f"""
+// The block loads the {nu} uniforms itself from `up` (the entry's u[] in memory, 8-byte aligned)
+// into fixed SGPRs (tools/gen_hash_asm.py --uload), so none of them is live outside it.
+"""
     if n_bar:
         prologue += f"""
 // {n_bar} s_barrier: every wave of the workgroup must run this function the same number of
@@ -1175,7 +1246,7 @@ static_assert(NPOW_ASM_N_UNIFORMS == {nu}, "include after the primary stream: th
 // VGPR window v{vbase}..v{vmax - 1}; {nu} uniform 64-bit values, {len(ops_in)} asm input operands;
 // modelled issue cost {est_cycles:.0f} SIMD cycles per wave (64 nonces).
 {prologue}
-__device__ __forceinline__ uint64_t {func}(uint64_t nonce, const uint64_t (&u)[NPOW_ASM_N_UNIFORMS]) {{
+__device__ __forceinline__ uint64_t {func}(uint64_t nonce, {"const uint64_t* up" if uload else "const uint64_t (&u)[NPOW_ASM_N_UNIFORMS]"}) {{
 #if defined(__HIP_DEVICE_COMPILE__)
   uint32_t value_lo, value_hi;
   asm{" volatile" if n_bar else ""}(
@@ -1185,7 +1256,7 @@ __device__ __forceinline__ uint64_t {func}(uint64_t nonce, const uint64_t (&u)[N
       : {clobbers});
   return ((uint64_t)value_hi << 32) | value_lo;
 #else
-  (void)nonce; (void)u;
+  (void)nonce; (void){"up" if uload else "u"};
   return 0;  // host compilation pass: device code is never executed here
 #endif
 }}
@@ -1203,6 +1274,8 @@ def main() -> int:
                     help="lockstep: an s_barrier after every N-th interval (0 = none; experiments)")
     ap.add_argument("--func", default="npow_asm_work_value",
                     help="device function name; any other name writes a device-only second stream (write_inc)")
+    ap.add_argument("--uload", type=int, default=-1,
+                    help="lockstep: the block loads its uniforms into SGPRs from this base on (uload_transform)")
     ap.add_argument("--shift", action="store_true", help="lockstep: the anti-phase stream (schedule_lockstep)")
     ap.add_argument("--pad-end", action="store_true", help="lockstep: a trailing s_barrier (pairs with --shift)")
     ap.add_argument("--lat", type=float, default=8.0, help="ilp: result latency (SIMD cycles)")
@@ -1300,12 +1373,24 @@ def main() -> int:
         if got != want:
             print(f"MISMATCH root={root.hex()} nonce={nonce:016x} got={got:016x} want={want:016x}")
             return 1
+    if args.uload >= 0:
+        lines = uload_transform(lines, args.uload, len(frontier))
+        for _ in range(args.check):  # the transformed stream, interpreted with its SGPR layout
+            root = bytes(rng.getrandbits(8) for _ in range(32))
+            nonce = rng.getrandbits(64)
+            words = [int.from_bytes(root[8 * i:8 * i + 8], "little") for i in range(4)]
+            got = interpret(lines, nonce, uniform_values(frontier, words))
+            want = int.from_bytes(hashlib.blake2b(nonce.to_bytes(8, "little") + root, digest_size=8).digest(), "little")
+            if got != want:
+                print(f"MISMATCH (uload) root={root.hex()} nonce={nonce:016x}")
+                return 1
     host_prog = c_expr_program(frontier)
     write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --add {args.add} --enc {args.enc}"
               + (f" --rotmad {args.rotmad}" if args.rotmad != "none" else "") + (" --swapmov" if args.swapmov else "")
               + (f" --lat {args.lat:g} --window {args.window}" if args.sched == "ilp" else "") + f" --pad {args.pad}"
               + (" --fuse-out none" if args.fuse_out == "none" else "")
-              + (f" --func {args.func}" if args.func != "npow_asm_work_value" else ""), est, args.func)
+              + (f" --func {args.func}" if args.func != "npow_asm_work_value" else "")
+              + (f" --uload {args.uload}" if args.uload >= 0 else ""), est, args.func)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
           f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")
     return 0
