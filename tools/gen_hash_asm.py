@@ -1390,7 +1390,9 @@ def main() -> int:
               + (f" --lat {args.lat:g} --window {args.window}" if args.sched == "ilp" else "") + f" --pad {args.pad}"
               + (" --fuse-out none" if args.fuse_out == "none" else "")
               + (f" --func {args.func}" if args.func != "npow_asm_work_value" else "")
-              + (f" --uload {args.uload}" if args.uload >= 0 else ""), est, args.func)
+              + (f" --uload {args.uload}" if args.uload >= 0 else "")
+              + (f" --base {args.base}" if args.base != 16 else "")
+              + (f" --limit {args.limit}" if args.limit != 64 else ""), est, args.func)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
           f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")
     return 0
