@@ -806,7 +806,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       const uint32_t verdict = __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const uint64_t dead = __hip_atomic_load(dead_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
-      const uint32_t it0 = it;
+      const uint32_t it0 = it;  // the poll phase
       const uint64_t value = npow_asm_work_value_lockstep_ld(nonce, c.up);
       ++it;
       bool hit = value >= c.threshold;
@@ -840,11 +840,16 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       }
       nonce += step;
       b += c.K;
+      // The verdict as read before this hash holds every request filed before it: each one was
+      // drained before the s_barrier below, which every wave passes before its next read.  So
+      // all waves see the same set and leave together, one hash after the request (pool_body_ls
+      // waits two: it has no barrier of its own between a request and the next read).
       const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(verdict);
-      if ((v >> 1) < it0) {  // the uniform verdict (pool_body_ls)
+      if (v != ~0u) {
         end = (v & 1) == 0;
         break;
       }
+      __builtin_amdgcn_s_barrier();
     }
     if (lane == 0 && done)
       atomicAdd(&st->done[c.slot][(w % kPoolDoneShards) * 8], (unsigned long long)done);
