@@ -292,6 +292,10 @@ SWAP_MOV = False
 LAT = 8.0
 ZPAIRS = 2  # {t, 0} pairs of the rotl1 trick in use at once (lockstep: one per G of a half-round, +2)
 BARRIER_LINES = ["s_barrier"]  # --sched lockstep: what ends an interval (+ "s_nop 0" keeps 8-byte parity)
+# --split (lockstep experiments): "order" puts an interval's 64-bit adds (v_lshl_add_u64, the rotl1
+# add included) after all its alignbits; "ad" also puts an s_barrier between the two runs; "fh" an
+# s_barrier between the full-rate and the half-rate part; "all" both barriers
+SPLIT = "none"
 
 
 def op_cost(op: Op) -> float:
@@ -366,19 +370,21 @@ def schedule_lockstep(ops: List[Op], shift: bool = False, pad_end: bool = False)
     for op in ops:
         by_g.setdefault(op.g, []).append(op)
     key: Dict[Tuple[int, str], Tuple[int, int]] = {}   # (op id, part) -> (interval, 0 = F / 1 = H)
+    dph = 2 if SPLIT != "none" else 1  # the adds' part: after the alignbits with --split
+    assert not (shift and dph == 2), "--shift and --split do not combine"
     for g, gops in by_g.items():
         L = 0
         base = 4 * (g // 4)  # 4 intervals per half-round
         for op in gops:
             if op.kind == "add":
-                key[(op.id, "all")] = (base + L, 1)
+                key[(op.id, "all")] = (base + L, dph)
             elif op.kind == "xrot32":
                 L += 1
                 key[(op.id, "all")] = (base + L, 0)
             elif op.kind == "xrot":
                 L += 1
                 key[(op.id, "F")] = (base + L, 0)
-                key[(op.id, "H")] = (base + L, 1)
+                key[(op.id, "H")] = (base + L, dph if (op.n == 63 and ROTL1_VIA_ADD) else 1)
             else:  # the output xor
                 key[(op.id, "all")] = (base + L + 1, 0)
     # dependencies win over the pattern: an op is never placed before what it reads
@@ -398,10 +404,14 @@ def schedule_lockstep(ops: List[Op], shift: bool = False, pad_end: bool = False)
     idx = {op.id: op for op in ops}
     items: list = []
     cur = None
-    for (oid, part), (iv, _ph) in units:
+    cur_ph = 0
+    for (oid, part), (iv, ph) in units:
         if cur is not None and iv != cur:
             items.append("BARRIER")
-        cur = iv
+        elif cur is not None and ph != cur_ph and (
+                (SPLIT in ("fh", "all") and cur_ph == 0) or (SPLIT in ("ad", "all") and cur_ph == 1 and ph == 2)):
+            items.append("BARRIER")
+        cur, cur_ph = iv, ph
         items.append((idx[oid], part) if part != "all" else idx[oid])
     if pad_end:
         items.append("BARRIER")
@@ -1276,6 +1286,8 @@ def main() -> int:
                     help="device function name; any other name writes a device-only second stream (write_inc)")
     ap.add_argument("--uload", type=int, default=-1,
                     help="lockstep: the block loads its uniforms into SGPRs from this base on (uload_transform)")
+    ap.add_argument("--split", choices=["none", "order", "ad", "fh", "all"], default="none",
+                    help="lockstep experiments: adds after alignbits within an interval (SPLIT)")
     ap.add_argument("--shift", action="store_true", help="lockstep: the anti-phase stream (schedule_lockstep)")
     ap.add_argument("--pad-end", action="store_true", help="lockstep: a trailing s_barrier (pairs with --shift)")
     ap.add_argument("--lat", type=float, default=8.0, help="ilp: result latency (SIMD cycles)")
@@ -1330,7 +1342,8 @@ def main() -> int:
         lines, vmax, counts = allocate_and_emit(order_i, vrs, args.base, args.limit, VOP3_SIMPLE)
     else:
         if args.sched == "lockstep":
-            global ZPAIRS, BARRIER_LINES
+            global ZPAIRS, BARRIER_LINES, SPLIT
+            SPLIT = args.split
             ZPAIRS = 6
             BARRIER_LINES = ["s_barrier", "s_nop 0"] if args.barrier_nop else ["s_barrier"]
             for op in reversed(ops):  # priorities are unused, but keep op.prio defined
@@ -1391,6 +1404,7 @@ def main() -> int:
               + (" --fuse-out none" if args.fuse_out == "none" else "")
               + (f" --func {args.func}" if args.func != "npow_asm_work_value" else "")
               + (f" --uload {args.uload}" if args.uload >= 0 else "")
+              + (f" --split {args.split}" if args.split != "none" else "")
               + (f" --base {args.base}" if args.base != 16 else "")
               + (f" --limit {args.limit}" if args.limit != 64 else ""), est, args.func)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
