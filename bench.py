@@ -802,14 +802,15 @@ def workload_burst(eng, args, rank, world, dist):
 
 def workload_sustained(eng, args, rank, world, dist):
     """BASELINE config 5: --duration seconds of fresh roots, --depth requests in flight per GPU."""
-    from collections import deque
     eng.reset_stats(0)
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    pending = deque()
+    pending = []
     nxt, nonces, ttw = 0, 0, []
     base = 9_000_000 + rank * 10_000_000
+    # every request is replaced as soon as it returns, whichever finishes first (polled every 0.2 ms:
+    # a FIFO wait on the oldest would leave the others' slots empty and count their queueing as ttw)
     while True:
         now = time.perf_counter()
         while len(pending) < args.depth and now - t0 < args.duration:
@@ -818,12 +819,19 @@ def workload_sustained(eng, args, rank, world, dist):
             pending.append((eng.submit(bench_root(i), SEND, start=bench_start(i), device_mask=1), now))
         if not pending:
             break
-        t, ts = pending.popleft()
-        r = t.wait()
-        if r.status != 0:
-            raise RuntimeError(f"sustained: status {r.status}")
-        nonces += r.nonces_done
-        ttw.append(time.perf_counter() - ts)
+        still = []
+        for t, ts in pending:
+            r = t.wait(0)
+            if r is None:
+                still.append((t, ts))
+                continue
+            if r.status != 0:
+                raise RuntimeError(f"sustained: status {r.status}")
+            nonces += r.nonces_done
+            ttw.append(time.perf_counter() - ts)
+        if len(still) == len(pending):
+            time.sleep(0.0002)
+        pending = still
     wall = time.perf_counter() - t0
     st = eng.stats(0)
     nonces, wall, ttw, (kms, kn, nl) = _reduce(dist, nonces, wall, ttw, (st.kernel_ms, st.nonces, st.launches))

@@ -67,7 +67,13 @@ typedef struct npow_device_stats {
   int32_t dead;           /* 1 once the device has been dropped: 3 invalid results in a row
                              (nano-work-server.exe @1669144) or a failed HIP call; searches then
                              skip it and its jobs' remaining ranges move to the other devices */
-  int32_t reserved;
+  int32_t pool_groups;    /* the search kernel: 0 = seq (NANOPOW_POOL_KERNEL=seq), 1 or 2 = lockstep
+                             workgroups per CU (npow_pool_kernel_ls* / _ls2*; NANOPOW_LS_GROUPS) */
+  uint64_t early_finishes;  /* jobs finished from the kernel's published final count (two-group
+                               kernels): a won or killed entry's count once no workgroup is left on
+                               it, before the launch that held it ends */
+  uint64_t early_mismatches; /* of those, counts that the read-back after the launch contradicted
+                               (always 0: a protocol check) */
 } npow_device_stats;
 
 /* Open every visible HIP device, create its stream and buffers.

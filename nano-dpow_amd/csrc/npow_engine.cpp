@@ -397,10 +397,21 @@ static double worker_cpu_ms(Device& d) {
   return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
 }
 
+// A job that finished early (npow_pool.cpp early_finish) returns before the launch that held it
+// is retired and counted; with no slot left searching, that launch ends within a hash, so the
+// stats calls wait (bounded) until the worker has retired everything and the counters are whole.
+static void settle_stats(const Device& d) {
+  const auto end = std::chrono::steady_clock::now() + std::chrono::milliseconds(200);
+  while (d.worker_busy.load(std::memory_order_acquire) && d.active_slots.load(std::memory_order_acquire) == 0 &&
+         !d.dead && std::chrono::steady_clock::now() < end)
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+}
+
 int npow_device_stats_get(int device, npow_device_stats* out) try {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size() || !out) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
   Device& d = *g_devs[device];
+  settle_stats(d);
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
   *out = npow_device_stats{};
@@ -414,6 +425,9 @@ int npow_device_stats_get(int device, npow_device_stats* out) try {
   out->host_cpu_ms = cpu - d.worker_cpu0_ms;
   out->host_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d.stats_t0).count();
   out->dead = d.dead ? 1 : 0;
+  out->pool_groups = pool_shape(d).lockstep ? pool_shape(d).groups : 0;
+  out->early_finishes = d.early;
+  out->early_mismatches = d.early_mismatch;
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 
@@ -421,9 +435,10 @@ int npow_device_stats_reset(int device) try {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size()) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
   Device& d = *g_devs[device];
+  settle_stats(d);
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
-  d.launches = d.nonces = d.invalid = 0;
+  d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = 0;
   d.kernel_ms = 0.0;
   d.clk_ticks = d.clk_ref_ticks = 0.0;
   d.stats_t0 = std::chrono::steady_clock::now();

@@ -56,6 +56,12 @@ struct Device {
   // statistics
   std::mutex stats_mu;
   uint64_t launches = 0, nonces = 0, invalid = 0;
+  uint64_t early = 0, early_mismatch = 0;  // jobs finished from a published final count (npow_pool.cpp)
+  // Published by the pool worker for npow_device_stats_get: it has launches or slots in flight, and
+  // how many of its slots are still searching.  A job finished early returns before the launch that
+  // held it is retired; with no slot searching, the stats wait for the worker to retire the rest.
+  std::atomic<bool> worker_busy{false};
+  std::atomic<int> active_slots{0};
   double kernel_ms = 0.0;
   double clk_ticks = 0.0, clk_ref_ticks = 0.0;  // in-kernel s_memtime / s_memrealtime spans (stats)
   std::chrono::steady_clock::time_point stats_t0 = std::chrono::steady_clock::now();

@@ -135,7 +135,11 @@ static_assert(sizeof(PoolTableArg) + 2 * sizeof(void*) <= 4096, "kernel argument
 
 struct PoolSlotWord {
   unsigned long long dead;  // highest generation known dead in this slot
-  uint8_t pad[56];
+  // Two-group kernels: workgroups on the slot's entry (npow_pool_kernel_ls2*; joins and leaves
+  // balance within every launch, so it is 0 between launches).  Once the entry is dead, whoever
+  // sees it at 0 publishes the slot's final nonce count (PoolMailbox::fin).
+  unsigned long long wgs;
+  uint8_t pad[48];
 };
 struct PoolDevState {
   PoolSlotWord slot[kMaxSlots];
@@ -158,8 +162,17 @@ struct PoolClk {
   uint64_t cycles, ref;
   uint32_t seq, pad;
 };
+// Final nonce count of a closed entry (two-group kernels): the sum of the slot's done shards once
+// no workgroup is left on it and none can join, so a won or killed job finishes without waiting
+// for its launch to end (the other entries may keep it running for the rest of its budget).
+struct alignas(64) PoolFin {
+  uint64_t gen;    // released after total
+  uint64_t total;  // the slot's done shards, summed (cumulative over its generations)
+  uint8_t pad[48];
+};
 struct PoolMailbox {
   PoolWin win[kMaxSlots];
+  PoolFin fin[kMaxSlots];
   uint64_t kill[kMaxSlots];  // kill[s] = gen: the job in slot s (that generation) must stop
   alignas(64) uint64_t yield;  // bumped by the host when new jobs wait for the next launch
   alignas(64) PoolClk clk[4][kClkWaves];  // [launch ring][XCD] (host: kEventRing == 4)

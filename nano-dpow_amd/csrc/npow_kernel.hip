@@ -747,13 +747,65 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
 // the uniforms it loads itself).  The loop keeps only what every iteration needs in registers:
 // the nonce advances in a VGPR by K * 64, the block index by K; the entry's fields, the table and
 // the mailbox are re-read inside the rare branches (a win, a poll, leaving an entry).
+//
+// Early finish: a won or killed entry usually shares its launch with live ones, which keep the
+// launch running for the rest of its budget; the job's nonce count would only be read back after
+// that.  Instead wave 0 of a workgroup joins an entry (adds 1 to the slot's wgs word) before its
+// waves hash it, and leaves it (subtracts 1) after all 16 waves have added their done counts.  An
+// entry is over once its dead word holds its generation (a win, a kill relay, a yield); a joiner
+// that then finds it dead leaves at once without hashing.  Whoever sees wgs at 0 after seeing the
+// entry dead -- the last leaver, or the marker itself -- sums the slot's done shards and publishes
+// the total (PoolMailbox::fin).  All of it is sequentially consistent at agent scope: a workgroup
+// that joins after that wgs read also finds the entry dead, and every hashing workgroup's done
+// adds precede its leave, so every published total is the final one (and equal, if two publish).
+// The host then finishes the job at once.  (A compare-and-swap join was measured: 512 workgroups
+// retrying on one word at every launch start cost 40 % of throughput.)
+__device__ __forceinline__ bool ls2_over(PoolDevState* st, uint32_t slot, uint64_t gen) {
+  return __hip_atomic_load(&st->slot[slot].dead, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT) >= gen;
+}
+__device__ __forceinline__ bool ls2_empty(PoolDevState* st, uint32_t slot) {
+  return __hip_atomic_load(&st->slot[slot].wgs, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT) == 0;
+}
+
+__device__ __forceinline__ void ls2_publish_fin(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
+  unsigned long long total = 0;
+#pragma unroll 4
+  for (int i = 0; i < kPoolDoneShards; ++i)
+    total += __hip_atomic_load(&st->done[slot][i * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&mb->fin[slot].total, (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&mb->fin[slot].gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Leave the entry (after the workgroup's done adds); the last one out of a dead entry publishes.
+__device__ __forceinline__ void ls2_leave(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
+  const unsigned long long old =
+      __hip_atomic_fetch_add(&st->slot[slot].wgs, ~0ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+  if (old == 1ull && ls2_over(st, slot, gen) && ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
+}
+
+// Join it unless it is over (then leave again at once, without hashing).
+__device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
+  __hip_atomic_fetch_add(&st->slot[slot].wgs, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+  if (!ls2_over(st, slot, gen)) return true;
+  ls2_leave(st, mb, slot, gen);
+  return false;
+}
+
+// Mark it dead (a win, a kill relay, a yield); with no workgroup on it, publish now.
+__device__ __forceinline__ void ls2_kill(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
+  __hip_atomic_fetch_max(&st->slot[slot].dead, (unsigned long long)gen, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+  if (ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
+}
+
 __device__ __noinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
                                              uint64_t wn, uint64_t wv) {
-  if (atomicMax(&st->slot[slot].dead, (unsigned long long)gen) < gen) {  // first win
+  if (__hip_atomic_fetch_max(&st->slot[slot].dead, (unsigned long long)gen, __ATOMIC_SEQ_CST,
+                             __HIP_MEMORY_SCOPE_AGENT) < gen) {  // first win
     PoolWin* pw = &mb->win[slot];
     __hip_atomic_store(&pw->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&pw->value, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&pw->gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    // the winner's own workgroup is on the entry: its leave publishes, after the win record
   }
 }
 
@@ -764,14 +816,31 @@ __device__ __noinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st, Po
   bool leave = false;
   if (__hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != tab->yield_base) {
     for (uint32_t k = 0; k < tab->n; ++k)
-      if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
+      if (!tab->e[k].bounded) ls2_kill(st, mb, tab->e[k].slot, tab->e[k].gen);
     leave = !pe->bounded;
   }
   if (__hip_atomic_load(&mb->kill[pe->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == pe->gen) {
-    atomicMax(&st->slot[pe->slot].dead, (unsigned long long)pe->gen);  // relay
+    ls2_kill(st, mb, pe->slot, pe->gen);  // relay
     leave = true;
   }
   return leave;
+}
+
+// Wave 0, lane 0: the entry the workgroup works on next -- e itself first at the launch's start
+// (its own entry, bounded or not), then the live unbounded entries cyclic from e + 1 -- joined;
+// n if none can be joined (the workgroup is finished).
+__device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
+                                          uint32_t k0) {
+  const uint32_t n = tab->n;
+  for (uint32_t k = k0; k < n; ++k) {
+    uint32_t e2 = e + k;
+    if (e2 >= n) e2 -= n;
+    const PoolEntry* pe = &tab->e[e2];
+    if (k > 0 && pe->bounded) continue;
+    if (load_dead(st, pe->slot) >= pe->gen) continue;
+    if (ls2_join(st, mb, pe->slot, pe->gen)) return e2;
+  }
+  return n;
 }
 
 template <bool BOUNDED>
@@ -786,12 +855,15 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   const uint32_t w = g * kLsWaves + wv;
   const uint32_t n = tab->n, iters = tab->iters;
   if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
+  if (threadIdx.x == 0) s_next = ls2_pick(tab, st, mb, g % n, 0);  // its own entry first
   __syncthreads();
   (void)s_flag;
 
-  uint32_t e = g % n, seg = 0, it = 0;
+  uint32_t e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+  uint32_t seg = 0, it = 0;
   bool end = false;
   for (;;) {
+    if (e == n) break;
     const PoolEntry* pe = &tab->e[e];
     PoolCursor c;
     pool_load_ls<true>(pe, c, g, wv, G, n, e, iters);
@@ -853,28 +925,17 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     }
     if (lane == 0 && done)
       atomicAdd(&st->done[c.slot][(w % kPoolDoneShards) * 8], (unsigned long long)done);
+    // every wave's add is performed before wave 0 leaves the entry (early finish, ls2_leave)
+    __threadfence();
+    __syncthreads();
+    if (wv == 0 && lane == 0) ls2_leave(st, mb, c.slot, c.gen);
     if (it >= iters || end) break;
-    if (wv == 0) {
-      uint32_t next = n;
-      for (uint32_t k = 1; k < n; ++k) {
-        uint32_t e2 = e + k;
-        if (e2 >= n) e2 -= n;
-        const PoolEntry* p2 = &tab->e[e2];
-        if (p2->bounded) continue;
-        if (load_dead(st, p2->slot) >= p2->gen) continue;
-        next = e2;
-        break;
-      }
-      if (lane == 0) {
-        s_next = next;
-        s_stop[(seg + 1) % 3] = ~0u;
-      }
+    if (wv == 0 && lane == 0) {
+      s_next = ls2_pick(tab, st, mb, e, 1);
+      s_stop[(seg + 1) % 3] = ~0u;
     }
     __syncthreads();
-    const uint32_t next =
-        __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (next == n) break;
-    e = next;
+    e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     ++seg;
   }
 }

@@ -263,6 +263,8 @@ struct Slot {
   bool no_more = false;    // bounded range fully issued
   bool readback = false;   // done-shard read-back queued (ev_done[slot] marks it)
   bool fresh = false;      // adopted since the last launch was built
+  bool fin_seen = false;   // the kernel published this generation's final count (PoolMailbox::fin) ...
+  bool early = false;      // ... and the job was finished from it before retiring
   struct Issued {
     uint64_t seq, base, count;
   };
@@ -301,6 +303,13 @@ class Worker {
   void yield_if_long();
   void handle_win(int s);
   bool win_published(int s) const;
+  void early_finish(int s);
+  void publish_busy() {
+    int active = 0;
+    for (const Slot& s : slots_) active += s.state == SlotState::kActive ? 1 : 0;
+    d_.active_slots.store(active, std::memory_order_release);
+    d_.worker_busy.store(busy(), std::memory_order_release);
+  }
   void check_slots();
   int launch();
   int queue_readbacks();
@@ -352,7 +361,7 @@ void Worker::adopt() {
     sl.job = j;
     sl.k = (size_t)k;
     sl.gen = ++g_gen;
-    sl.win_seen = sl.requeue = sl.no_more = sl.readback = false;
+    sl.win_seen = sl.requeue = sl.no_more = sl.readback = sl.fin_seen = sl.early = false;
     sl.fresh = true;
     sl.inflight.clear();
     j->on_dev[k] = 1;
@@ -466,6 +475,31 @@ bool Worker::win_published(int s) const {
   return !sl.win_seen && __atomic_load_n(&d_.pmb->win[s].gen, __ATOMIC_ACQUIRE) == sl.gen;
 }
 
+// The kernel published slot s's final nonce count (two-group kernels, npow_kernel.hip "Early
+// finish"): no workgroup is on the entry and none can join it, so a decided job is finished now
+// instead of after the launch -- which its other entries may keep running for the rest of its
+// budget.  A yielded entry (the job is re-adopted) or an invalid win (re-armed) waits for retire().
+void Worker::early_finish(int s) {
+  Slot& sl = slots_[s];
+  sl.fin_seen = true;
+  if (win_published(s)) handle_win(s);  // the winner released its record before closing the entry
+  const uint64_t total = __atomic_load_n(&d_.pmb->fin[s].total, __ATOMIC_RELAXED);
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  Job& j = *sl.job;
+  if (d_.dead || sl.requeue || !j.decided.load()) return;
+  sl.early = true;
+  const uint64_t delta = total - sl.baseline;
+  sl.baseline = total;  // retire() then reads back the same total: a delta of 0
+  j.done += delta;
+  if (g_trace_lat && j.t_kend == 0) j.t_kend = now_us();
+  {
+    std::lock_guard<std::mutex> sg(d_.stats_mu);
+    d_.nonces += delta;
+    d_.early++;
+  }
+  device_done_locked(sl.job, sl.k);
+}
+
 void Worker::check_slots() {
   for (int s = 0; s < kMaxSlots; ++s) {
     Slot& sl = slots_[s];
@@ -494,6 +528,13 @@ void Worker::check_slots() {
     } else if (sl.no_more) {
       sl.state = SlotState::kDraining;
     }
+  }
+  publish_busy();  // before a job can finish early: its waiter may read the stats at once
+  for (int s = 0; s < kMaxSlots; ++s) {
+    const Slot& sl = slots_[s];
+    if (sl.state == SlotState::kDraining && !sl.fin_seen &&
+        __atomic_load_n(&d_.pmb->fin[s].gen, __ATOMIC_ACQUIRE) == sl.gen)
+      early_finish(s);
   }
 }
 
@@ -642,9 +683,16 @@ int Worker::retire() {
       d_.nonces += delta;
     }
     if (win_published(s)) handle_win(s);  // published by the last launch, not yet seen
-    NPOW_DBG("nanopow[%d]: retire slot %d g%llu done %llu requeue %d\n", d_.id, s, (unsigned long long)sl.gen,
-             (unsigned long long)delta, (int)sl.requeue);
-    {
+    NPOW_DBG("nanopow[%d]: retire slot %d g%llu done %llu requeue %d early %d\n", d_.id, s,
+             (unsigned long long)sl.gen, (unsigned long long)delta, (int)sl.requeue, (int)sl.early);
+    if (sl.early) {  // finished by early_finish(): the read-back must add nothing to its count
+      if (delta != 0) {
+        fprintf(stderr, "nanopow: GPU %d slot %d: read back %llu nonces past the published final count\n", d_.id,
+                s, (unsigned long long)delta);
+        std::lock_guard<std::mutex> sg(d_.stats_mu);
+        d_.early_mismatch++;
+      }
+    } else {
       std::lock_guard<std::mutex> g(g_pool.mu);
       Job& j = *sl.job;
       j.done += delta;
@@ -691,6 +739,7 @@ int Worker::step() {
   if (d_.tasks_waiting.load() == 0)            // a sweep / values call is waiting: drain instead
     if (int rc = launch()) return rc;
   if (int rc = retire()) return rc;
+  publish_busy();
   return NPOW_OK;
 }
 
@@ -717,6 +766,7 @@ void Worker::run() {
     }
     if (!busy()) adopt();  // jobs admitted since the last look
     if (!busy()) {
+      publish_busy();
       if (dev_lock_.owns_lock()) dev_lock_.unlock();
       // Spin a little before sleeping: a serial client submits its next request a few tens of
       // microseconds after the last one ends, and a condition-variable wake-up costs about as

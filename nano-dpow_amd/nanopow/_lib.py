@@ -61,7 +61,9 @@ class DeviceStats(ctypes.Structure):
         ("host_cpu_ms", ctypes.c_double),
         ("host_wall_ms", ctypes.c_double),
         ("dead", ctypes.c_int32),
-        ("reserved", ctypes.c_int32),
+        ("pool_groups", ctypes.c_int32),
+        ("early_finishes", ctypes.c_uint64),
+        ("early_mismatches", ctypes.c_uint64),
     ]
 
 
@@ -347,6 +349,10 @@ class Engine:
         s = DeviceStats()
         _check(self.lib.npow_device_stats_get(device, ctypes.byref(s)), self.lib)
         return s
+
+    def pool_kernel_groups(self, device: int = 0) -> int:
+        """The search kernel in use: 0 = seq, 1 / 2 = lockstep workgroups per CU (2: early finish)."""
+        return int(self.stats(device).pool_groups)
 
     def reset_stats(self, device: int = 0) -> None:
         _check(self.lib.npow_device_stats_reset(device), self.lib)
