@@ -74,6 +74,8 @@ typedef struct npow_device_stats {
                                it, before the launch that held it ends */
   uint64_t early_mismatches; /* of those, counts that the read-back after the launch contradicted
                                (always 0: a protocol check) */
+  uint64_t yields;          /* running launches ended early so that new jobs could start */
+  uint64_t dyn_entries;     /* jobs that joined a running two-group launch instead (no yield) */
 } npow_device_stats;
 
 /* Open every visible HIP device, create its stream and buffers.

@@ -428,6 +428,8 @@ int npow_device_stats_get(int device, npow_device_stats* out) try {
   out->pool_groups = pool_shape(d).lockstep ? pool_shape(d).groups : 0;
   out->early_finishes = d.early;
   out->early_mismatches = d.early_mismatch;
+  out->yields = d.yields;
+  out->dyn_entries = d.dyn;
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 
@@ -438,7 +440,7 @@ int npow_device_stats_reset(int device) try {
   settle_stats(d);
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
-  d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = 0;
+  d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = 0;
   d.kernel_ms = 0.0;
   d.clk_ticks = d.clk_ref_ticks = 0.0;
   d.stats_t0 = std::chrono::steady_clock::now();

@@ -57,6 +57,7 @@ struct Device {
   std::mutex stats_mu;
   uint64_t launches = 0, nonces = 0, invalid = 0;
   uint64_t early = 0, early_mismatch = 0;  // jobs finished from a published final count (npow_pool.cpp)
+  uint64_t yields = 0, dyn = 0;            // launches yielded / jobs that joined a running launch
   // Published by the pool worker for npow_device_stats_get: it has launches or slots in flight, and
   // how many of its slots are still searching.  A job finished early returns before the launch that
   // held it is retired; with no slot searching, the stats wait for the worker to retire the rest.

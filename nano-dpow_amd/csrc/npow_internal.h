@@ -107,6 +107,7 @@ struct PoolEntry {
   uint32_t slot;     // device slot index (PoolDevState / PoolMailbox arrays)
   uint32_t bounded;  // 1: dense mapping over the entry's own waves, no migrants
 };
+static_assert(offsetof(PoolEntry, u) == 0, "the two-group kernel finds an entry from its uniforms' address");
 struct PoolTable {
   uint32_t n;          // entries in use (1..kMaxSlots)
   uint32_t poll_mask;  // a wave reads the host kill word when ((it + w) & poll_mask) == 0
@@ -114,11 +115,13 @@ struct PoolTable {
   uint32_t budget;     // > 0: a wave on an unbounded entry stops once this many 100-MHz
                        // s_memrealtime ticks have passed since it started (all waves stop
                        // together); 0 = iteration count only
-  uint64_t yield_base;    // PoolMailbox::yield when the table was built: a polling wave that
-                          // reads a different value ends the launch's unbounded entries
+  uint64_t yield_base;    // PoolMailbox::ctl when the table was built: a polling wave that reads
+                          // a different high half ends the launch's unbounded entries
   uint32_t ring;          // PoolMailbox::clk[ring]: this launch's clock records ...
   uint32_t seq;           // ... tagged with the launch's sequence number (low 32 bits)
-  uint32_t pad[8];
+  uint32_t dyn_base;      // two-group kernels: the low half of PoolMailbox::ctl when the table was built -- the
+                          // launch may also search the entries the host publishes after it
+  uint32_t pad[7];
   PoolEntry e[kMaxSlots];
 };
 inline size_t pool_table_bytes(uint32_t n) { return offsetof(PoolTable, e) + (size_t)n * sizeof(PoolEntry); }
@@ -170,11 +173,27 @@ struct alignas(64) PoolFin {
   uint64_t total;  // the slot's done shards, summed (cumulative over its generations)
   uint8_t pad[48];
 };
+// An unbounded job adopted while a two-group launch runs joins that launch instead of ending it
+// (a yield): the host writes its entry at ring position p (dyn[p % kDynEntries]) and then releases
+// the low half of PoolMailbox::ctl = p + 1; the launch's entries are its table's n entries followed by positions
+// dyn_base.. of the ring, and workgroups move to a new entry as they rebalance (npow_kernel.hip).
+// Each entry has cache lines of its own, and a position is written at most once while a launch
+// that can read it runs, so no scalar-cache line can hold an older entry there.
+constexpr int kDynEntries = 32;
+struct alignas(64) PoolDynEntry {
+  PoolEntry e;
+  uint8_t pad[192 - sizeof(PoolEntry)];
+};
+static_assert(sizeof(PoolDynEntry) == 192, "3 cache lines per dynamic entry");
 struct PoolMailbox {
   PoolWin win[kMaxSlots];
   PoolFin fin[kMaxSlots];
+  PoolDynEntry dyn[kDynEntries];
   uint64_t kill[kMaxSlots];  // kill[s] = gen: the job in slot s (that generation) must stop
-  alignas(64) uint64_t yield;  // bumped by the host when new jobs wait for the next launch
+  // High half: bumped by the host when new jobs wait for the next launch (a yield); low half: the
+  // dynamic entries published (ring positions, see PoolDynEntry).  One word, so a poll reads both
+  // with one uncached read.
+  alignas(64) uint64_t ctl;
   alignas(64) PoolClk clk[4][kClkWaves];  // [launch ring][XCD] (host: kEventRing == 4)
 };
 

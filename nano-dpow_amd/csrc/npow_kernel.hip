@@ -108,6 +108,9 @@ __device__ __forceinline__ uint64_t work_value_full(uint64_t nonce, const uint64
   return kH0 ^ v[0] ^ v[8];
 }
 
+__device__ __forceinline__ uint64_t uni64(uint64_t x) {  // a wave-uniform value, in SGPRs
+  return pack(__builtin_amdgcn_readfirstlane((uint32_t)x), __builtin_amdgcn_readfirstlane((uint32_t)(x >> 32)));
+}
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, int lane) {
   const uint32_t lo = __builtin_amdgcn_readlane((int)(uint32_t)x, lane);
   const uint32_t hi = __builtin_amdgcn_readlane((int)(uint32_t)(x >> 32), lane);
@@ -445,7 +448,7 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
   const uint32_t w = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
   const uint32_t W = gridDim.x * (kBlock / 64);
   const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask, budget = tab->budget;
-  const uint64_t yield_base = tab->yield_base;  // read once: the loop below compares against it
+  const uint64_t yield_base = tab->yield_base >> 32;  // read once: the loop below compares against it
   unsigned long long* const done_base = &st->done[0][(blockIdx.x % kPoolDoneShards) * 8];
   // Time budget.  VALU issue on a SIMD goes to its OLDEST wave first (MI355X_MICROARCH.md:
   // priority, then age), so the 8 waves of a SIMD do not progress together: the oldest runs
@@ -478,7 +481,7 @@ __device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, Poo
       uint64_t kill, yld;
       if (__builtin_expect(poll, 0)) {
         kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        yld = __hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        yld = __hip_atomic_load(&mb->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32;
       }
 
       const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;  // consumed after the hash
@@ -627,7 +630,7 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
   const uint32_t g = blockIdx.x, G = gridDim.x;
   const uint32_t w = g * kLsWaves + wv;
   const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask, budget = tab->budget;
-  const uint64_t yield_base = tab->yield_base;
+  const uint64_t yield_base = tab->yield_base >> 32;
   unsigned long long* const done_base = &st->done[0][(w % kPoolDoneShards) * 8];
   if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
   __syncthreads();
@@ -649,7 +652,7 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
       uint64_t kill, yld;
       if (__builtin_expect(poll, 0)) {
         kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        yld = __hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        yld = __hip_atomic_load(&mb->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32;
       }
       const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
       const uint32_t it0 = it;
@@ -797,7 +800,7 @@ __device__ __forceinline__ void ls2_kill(PoolDevState* st, PoolMailbox* mb, uint
   if (ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
 }
 
-__device__ __noinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
+__device__ __forceinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
                                              uint64_t wn, uint64_t wv) {
   if (__hip_atomic_fetch_max(&st->slot[slot].dead, (unsigned long long)gen, __ATOMIC_SEQ_CST,
                              __HIP_MEMORY_SCOPE_AGENT) < gen) {  // first win
@@ -809,38 +812,100 @@ __device__ __noinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* mb, 
   }
 }
 
+// The launch's entries: the table's n, then the dynamic entries the host has published since the
+// table was built (PoolMailbox::dyn, at most kDynEntries; n + their count <= kMaxSlots, one slot
+// each).  kNoEntry: none.
+constexpr uint32_t kNoEntry = 0xffffffffu;
+// Through the constant address space: the launch's entries do not change while it can read them,
+// and the table's and the ring's fields then load with scalar loads into SGPRs alike.
+typedef const __attribute__((address_space(4))) PoolEntry ConstEntry;
+__device__ __forceinline__ ConstEntry* ls2_entry(const PoolTable* tab, const PoolMailbox* mb, uint32_t e) {
+  const PoolEntry* p = e < tab->n ? &tab->e[e] : &mb->dyn[(tab->dyn_base + (e - tab->n)) % kDynEntries].e;
+  return (ConstEntry*)(uintptr_t)p;
+}
+__device__ __forceinline__ uint64_t ls2_ctl(PoolMailbox* mb) {
+  return __hip_atomic_load(&mb->ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint32_t ls2_dyn_count(const PoolTable* tab, uint64_t ctl) {
+  const uint32_t d = (uint32_t)ctl - tab->dyn_base;
+  return d < (uint32_t)kDynEntries ? d : (uint32_t)kDynEntries;
+}
+__device__ __forceinline__ unsigned long long ls2_wgs(PoolDevState* st, uint32_t slot) {
+  return __hip_atomic_load(&st->slot[slot].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // A polling wave (lane 0 only): the host words of the entry.  Returns true when the wave's
-// workgroup must leave the entry (new jobs wait and the entry is unbounded, or it was killed).
-__device__ __noinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e) {
-  const PoolEntry* pe = &tab->e[e];
+// workgroup must leave the entry: new jobs wait and the entry is unbounded (a yield), it was
+// killed, or it is unbounded and a dynamic entry has at least two workgroups fewer than it (the
+// workgroup moves there: a job that joined the running launch collects its share a workgroup at a
+// time, each from the most crowded entry among the pollers).
+__device__ __forceinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e) {
+  const ConstEntry* pe = ls2_entry(tab, mb, e);
+  const uint64_t ctl = ls2_ctl(mb);
+  const uint32_t nd = ls2_dyn_count(tab, ctl);
   bool leave = false;
-  if (__hip_atomic_load(&mb->yield, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != tab->yield_base) {
-    for (uint32_t k = 0; k < tab->n; ++k)
-      if (!tab->e[k].bounded) ls2_kill(st, mb, tab->e[k].slot, tab->e[k].gen);
+  if ((ctl >> 32) != (tab->yield_base >> 32)) {
+    for (uint32_t k = 0; k < tab->n + nd; ++k) {
+      ConstEntry* q = ls2_entry(tab, mb, k);
+      if (!q->bounded) ls2_kill(st, mb, q->slot, q->gen);
+    }
     leave = !pe->bounded;
   }
   if (__hip_atomic_load(&mb->kill[pe->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == pe->gen) {
     ls2_kill(st, mb, pe->slot, pe->gen);  // relay
     leave = true;
   }
+  if (!leave && !pe->bounded && nd > 0) {
+    const unsigned long long mine = ls2_wgs(st, pe->slot);
+    for (uint32_t k = tab->n; k < tab->n + nd && !leave; ++k) {
+      if (k == e) continue;
+      ConstEntry* q = ls2_entry(tab, mb, k);
+      leave = load_dead(st, q->slot) < q->gen && ls2_wgs(st, q->slot) + 2 <= mine;
+    }
+  }
   return leave;
 }
 
-// Wave 0, lane 0: the entry the workgroup works on next -- e itself first at the launch's start
-// (its own entry, bounded or not), then the live unbounded entries cyclic from e + 1 -- joined;
-// n if none can be joined (the workgroup is finished).
+// Wave 0 (every lane): the entry the workgroup works on next, joined; kNoEntry if none can be.  At
+// the launch's start (first) its own entry e, bounded or not, if it can be joined; otherwise the
+// live unbounded entry with the fewest workgroups, ties broken by a hash of the workgroup index so
+// that the workgroups leaving one entry spread over the others.  Each lane looks at one entry.
 __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
-                                          uint32_t k0) {
-  const uint32_t n = tab->n;
-  for (uint32_t k = k0; k < n; ++k) {
-    uint32_t e2 = e + k;
-    if (e2 >= n) e2 -= n;
-    const PoolEntry* pe = &tab->e[e2];
-    if (k > 0 && pe->bounded) continue;
-    if (load_dead(st, pe->slot) >= pe->gen) continue;
-    if (ls2_join(st, mb, pe->slot, pe->gen)) return e2;
+                                          bool first) {
+  const uint32_t lane = threadIdx.x & 63, g = blockIdx.x;
+  if (first) {
+    uint32_t ok = 0;
+    if (lane == 0) {
+      ConstEntry* pe = ls2_entry(tab, mb, e);
+      ok = load_dead(st, pe->slot) < pe->gen && ls2_join(st, mb, pe->slot, pe->gen) ? 1u : 0u;
+    }
+    if (__builtin_amdgcn_readfirstlane(ok)) return e;
   }
-  return n;
+  const uint32_t N = tab->n + ls2_dyn_count(tab, ls2_ctl(mb));  // <= kMaxSlots = 64: one lane each
+  for (int attempt = 0; attempt < 4; ++attempt) {
+    unsigned long long key = ~0ull;
+    if (lane < N && lane != e) {
+      ConstEntry* q = ls2_entry(tab, mb, lane);
+      if (!q->bounded && load_dead(st, q->slot) < q->gen) {
+        const uint32_t tie = ((lane + 1u) * 0x9e3779b1u) ^ (g * 0x85ebca6bu);
+        key = (ls2_wgs(st, q->slot) << 32) | (tie & ~63u) | lane;
+      }
+    }
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+      const unsigned long long o = __shfl_xor(key, m);
+      key = o < key ? o : key;
+    }
+    if (key == ~0ull) return kNoEntry;
+    const uint32_t pick = (uint32_t)key & 63u;
+    uint32_t ok = 0;
+    if (lane == 0) {
+      ConstEntry* q = ls2_entry(tab, mb, pick);
+      ok = ls2_join(st, mb, q->slot, q->gen) ? 1u : 0u;
+    }
+    if (__builtin_amdgcn_readfirstlane(ok)) return pick;
+  }
+  return kNoEntry;  // entries died under every attempt: the workgroup is finished
 }
 
 template <bool BOUNDED>
@@ -855,7 +920,10 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   const uint32_t w = g * kLsWaves + wv;
   const uint32_t n = tab->n, iters = tab->iters;
   if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
-  if (threadIdx.x == 0) s_next = ls2_pick(tab, st, mb, g % n, 0);  // its own entry first
+  if (wv == 0) {
+    const uint32_t first = ls2_pick(tab, st, mb, g % n, true);  // its own entry first
+    if (lane == 0) s_next = first;
+  }
   __syncthreads();
   (void)s_flag;
 
@@ -863,8 +931,8 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   uint32_t seg = 0, it = 0;
   bool end = false;
   for (;;) {
-    if (e == n) break;
-    const PoolEntry* pe = &tab->e[e];
+    if (e == kNoEntry) break;
+    const PoolEntry* pe = (const PoolEntry*)ls2_entry(tab, mb, e);
     PoolCursor c;
     pool_load_ls<true>(pe, c, g, wv, G, n, e, iters);
     const uint32_t sw = seg % 3;
@@ -879,9 +947,10 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       const uint64_t dead = __hip_atomic_load(dead_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
       const uint32_t it0 = it;  // the poll phase
+      const uint64_t thr = c.threshold, gen = c.gen;
       const uint64_t value = npow_asm_work_value_lockstep_ld(nonce, c.up);
       ++it;
-      bool hit = value >= c.threshold;
+      bool hit = value >= thr;
       if constexpr (BOUNDED) {
         const uint32_t in_lanes = b < c.last_b ? 64u : (b == c.last_b ? c.tail : 0u);
         hit = hit && lane < in_lanes;
@@ -902,7 +971,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
         leave = leave || __builtin_amdgcn_readfirstlane(
                              __hip_atomic_load(&s_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) != 0;
       }
-      leave = leave || readlane64(dead, 0) == c.gen;
+      leave = leave || readlane64(dead, 0) == gen;
       const bool late = budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget;
       if (__builtin_expect(leave || late, 0)) {
         if (lane == 0)
@@ -930,9 +999,12 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     __syncthreads();
     if (wv == 0 && lane == 0) ls2_leave(st, mb, c.slot, c.gen);
     if (it >= iters || end) break;
-    if (wv == 0 && lane == 0) {
-      s_next = ls2_pick(tab, st, mb, e, 1);
-      s_stop[(seg + 1) % 3] = ~0u;
+    if (wv == 0) {
+      const uint32_t next = ls2_pick(tab, st, mb, e, false);
+      if (lane == 0) {
+        s_next = next;
+        s_stop[(seg + 1) % 3] = ~0u;
+      }
     }
     __syncthreads();
     e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));

@@ -62,6 +62,7 @@ constexpr double kYieldMinUs = 1500.0;  // yield a running launch only if more b
 constexpr int kYieldMaxLive = 8;
 constexpr int kIdleSpinUs = 2000;       // an idle worker polls for new jobs this long before sleeping
 constexpr double kPrelaunchUs = 2000.0;  // queue the next launch when the running one has this much budget left
+constexpr double kDynMinUs = 3000.0;     // join a running launch only with this much budget left
 constexpr double kFreshSpinUs = 400.0;   // poll without sleeping this long after a launch starts (quick wins)
 constexpr int kInvalidStreakMax = 3;     // consecutive invalid results that drop a device (@1669144)
 // Between steps a worker with a launch in flight sleeps this long (wakes early on new jobs):
@@ -263,6 +264,7 @@ struct Slot {
   bool no_more = false;    // bounded range fully issued
   bool readback = false;   // done-shard read-back queued (ev_done[slot] marks it)
   bool fresh = false;      // adopted since the last launch was built
+  bool new_job = false;    // adopted for the first time on this device (not a re-adoption)
   bool fin_seen = false;   // the kernel published this generation's final count (PoolMailbox::fin) ...
   bool early = false;      // ... and the job was finished from it before retiring
   struct Issued {
@@ -274,6 +276,8 @@ struct Slot {
 struct PoolInflight {
   uint64_t seq;
   int ring;
+  uint64_t dyn_base;    // PoolTable::dyn_base of the launch
+  uint64_t yield_base;  // PoolTable::yield_base of the launch
 };
 
 class Worker {
@@ -290,6 +294,7 @@ class Worker {
   int ring_ = 0;
   std::chrono::steady_clock::time_point front_start_{};  // host estimate of the running launch's start
   uint64_t yields_ = 0;
+  uint64_t ctl_ = 0;  // PoolMailbox::ctl (only this worker writes it): yields << 32 | dynamic entries
   int invalid_streak_ = 0;  // consecutive winners of this device that failed CPU re-validation
   std::unique_lock<std::mutex> dev_lock_{d_.mu, std::defer_lock};
 
@@ -301,6 +306,7 @@ class Worker {
   }
   void adopt();
   void yield_if_long();
+  bool dyn_add(int s);
   void handle_win(int s);
   bool win_published(int s) const;
   void early_finish(int s);
@@ -366,10 +372,71 @@ void Worker::adopt() {
     sl.inflight.clear();
     j->on_dev[k] = 1;
     if (g_trace_lat && j->t_adopt == 0) j->t_adopt = now_us();
-    if (!j->seen_dev[k]) adopted = true;  // a new job: worth ending a long launch for
+    sl.new_job = !j->seen_dev[k];
+    if (sl.new_job) adopted = true;  // a new job: worth ending a long launch for
     j->seen_dev[k] = 1;
   }
-  if (adopted) yield_if_long();
+  // Unbounded jobs join the running two-group launch as dynamic entries (no yield: the launch goes
+  // on and workgroups move to them); a new job that cannot ends the long launch instead.
+  bool waiting_new = false;
+  for (int s = 0; s < kMaxSlots; ++s) {
+    Slot& sl = slots_[s];
+    if (sl.state != SlotState::kActive || !sl.fresh) continue;
+    if (!dyn_add(s) && sl.new_job) waiting_new = true;
+  }
+  if (adopted && waiting_new) yield_if_long();
+}
+
+// Publish the job of fresh slot s as a dynamic entry of the running launch (npow_internal.h
+// PoolDynEntry; two-group kernels only): exactly one launch in flight, enough of its budget left,
+// not yielded, a free ring position, an unbounded job with a full region left.  Its region is taken
+// from the job's queue as launch() would, and counts as part of the running launch.  Caller holds
+// g_pool.mu (adopt()).
+bool Worker::dyn_add(int s) {
+  Slot& sl = slots_[s];
+  Job& j = *sl.job;
+  if (q_.size() != 1 || j.max_per_dev || g_budget_us.load() == 0) return false;
+  const PoolShape sh = pool_shape(d_);
+  if (!sh.lockstep || sh.groups != 2) return false;
+  const PoolInflight& f = q_.front();
+  if ((uint32_t)((uint32_t)ctl_ - (uint32_t)f.dyn_base) >= (uint32_t)kDynEntries) return false;
+  if ((ctl_ >> 32) != (f.yield_base >> 32)) return false;  // it is ending
+  bool other = false;  // another live entry keeps the launch running (workgroups to move)
+  for (int k = 0; k < kMaxSlots && !other; ++k)
+    other = k != s && slots_[k].state == SlotState::kActive && !slots_[k].fresh;
+  if (!other) return false;  // they are leaving: the next launch, right after, takes the job
+  const double left_us = g_budget_us.load() - std::chrono::duration<double, std::micro>(
+                                                  std::chrono::steady_clock::now() - front_start_).count();
+  if (left_us < kDynMinUs) return false;  // the next launch, queued soon, takes it
+  const uint32_t iters = sh.launch_iters(g_iters.load());
+  const uint64_t full = sh.full(iters);
+  std::deque<Range>& todo = j.todo[sl.k];
+  if (todo.empty() || todo.front().count < full) return false;
+  PoolEntry& pe = d_.pmb->dyn[(uint32_t)ctl_ % kDynEntries].e;
+  memcpy(pe.u, j.u, sizeof(pe.u));
+  pe.threshold = j.threshold;
+  pe.gen = sl.gen;
+  pe.slot = (uint32_t)s;
+  pe.bounded = 0;
+  Range& r = todo.front();
+  pe.base = r.base;
+  pe.count = full;
+  r.base += full;
+  r.count -= full;
+  if (r.count == 0) todo.pop_front();
+  sl.inflight.push_back({f.seq, pe.base, pe.count});
+  if (todo.empty()) sl.no_more = true;
+  sl.fresh = false;
+  if (g_trace_lat && j.t_launch == 0) j.t_launch = now_us();
+  ctl_ = (ctl_ & ~0xffffffffull) | (uint32_t)(ctl_ + 1);  // the low half wraps on its own
+  __atomic_store_n(&d_.pmb->ctl, ctl_, __ATOMIC_RELEASE);  // after the entry
+  {
+    std::lock_guard<std::mutex> sg(d_.stats_mu);
+    d_.dyn++;
+  }
+  NPOW_DBG("nanopow[%d]: dynamic entry %u: slot %d g%llu in launch %llu\n", d_.id, (uint32_t)ctl_ - 1u,
+           s, (unsigned long long)sl.gen, (unsigned long long)f.seq);
+  return true;
 }
 
 // New jobs wait for the next launch's table.  Launches run for a long time budget (their
@@ -396,8 +463,11 @@ void Worker::yield_if_long() {
   }
   NPOW_DBG("nanopow[%d]: yield %s\n", d_.id, any ? "raised" : "(no slot to hand back)");
   if (any) {
-    __atomic_store_n(&d_.pmb->yield, __atomic_load_n(&d_.pmb->yield, __ATOMIC_RELAXED) + 1, __ATOMIC_RELEASE);
+    ctl_ += 1ull << 32;
+    __atomic_store_n(&d_.pmb->ctl, ctl_, __ATOMIC_RELEASE);
     ++yields_;
+    std::lock_guard<std::mutex> sg(d_.stats_mu);
+    d_.yields++;
   }
 }
 
@@ -560,7 +630,8 @@ int Worker::launch() {
   t.poll_mask = poll_mask();
   t.iters = iters;
   t.budget = g_budget_us.load() * 100u;  // s_memrealtime runs at 100 MHz
-  t.yield_base = __atomic_load_n(&d_.pmb->yield, __ATOMIC_ACQUIRE);
+  t.yield_base = ctl_;
+  t.dyn_base = (uint32_t)ctl_;
   ++seq_;
   t.ring = (uint32_t)ring_;
   t.seq = (uint32_t)seq_;
@@ -621,7 +692,7 @@ int Worker::launch() {
   NPOW_DBG("nanopow[%d]: launch %llu n=%u slots:", d_.id, (unsigned long long)seq_, n);
   for (uint32_t e = 0; e < n; ++e) NPOW_DBG(" %d/g%llu", idx[e], (unsigned long long)t.e[e].gen);
   NPOW_DBG("\n");
-  q_.push_back({seq_, r});
+  q_.push_back({seq_, r, (uint32_t)ctl_, t.yield_base});
   return NPOW_OK;
 }
 

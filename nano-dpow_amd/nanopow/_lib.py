@@ -64,6 +64,8 @@ class DeviceStats(ctypes.Structure):
         ("pool_groups", ctypes.c_int32),
         ("early_finishes", ctypes.c_uint64),
         ("early_mismatches", ctypes.c_uint64),
+        ("yields", ctypes.c_uint64),
+        ("dyn_entries", ctypes.c_uint64),
     ]
 
 

@@ -224,6 +224,9 @@ def test_new_job_does_not_wait_for_a_long_launch(gpu_engine):
             assert sorted(lat)[len(lat) // 2] < 0.01, lat
             st = gpu_engine.stats(0)
             assert st.early_finishes >= len(lat) and st.early_mismatches == 0
+            # each new job joined the busy job's running launch as a dynamic entry: no launch ended
+            # early for it (the first launch may have been too close to its end to take one)
+            assert st.dyn_entries >= len(lat) - 1 and st.yields <= 1, (st.dyn_entries, st.yields)
         assert busy.wait(0) is None  # still searching after being handed back
         tok.set()
         res = busy.wait(10)
