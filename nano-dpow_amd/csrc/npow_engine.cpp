@@ -317,6 +317,7 @@ int npow_init(int* n_devices) try {
   if (const char* k = getenv("NANOPOW_POOL_KERNEL")) g_pool_lockstep = strcmp(k, "seq") != 0;
   if (const char* l = getenv("NANOPOW_LS_LDS")) g_ls_lds = (uint32_t)atoi(l);
   if (const char* k = getenv("NANOPOW_LS_GROUPS")) g_ls_groups = atoi(k) == 1 ? 1 : 2;
+  if (const char* b = getenv("NANOPOW_BUDGET_US")) g_budget_us = (uint32_t)atoi(b);  // A/B runs
   int n_logical = n;
   if (const char* v = getenv("NANOPOW_VIRTUAL_DEVICES")) {
     const int k = atoi(v);

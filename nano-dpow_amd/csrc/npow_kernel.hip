@@ -914,6 +914,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   __shared__ uint32_t s_stop[3];  // per entry segment (mod 3): the earliest stop request (pool_body_ls)
   __shared__ uint32_t s_flag;     // lane 0 of a polling wave -> its wave: leave the entry
   __shared__ uint32_t s_next;
+  __shared__ uint32_t s_done[kLsWaves];  // each wave's nonces on the entry it is leaving
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t g = blockIdx.x, G = gridDim.x;
@@ -992,12 +993,19 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       }
       __builtin_amdgcn_s_barrier();
     }
-    if (lane == 0 && done)
-      atomicAdd(&st->done[c.slot][(w % kPoolDoneShards) * 8], (unsigned long long)done);
-    // every wave's add is performed before wave 0 leaves the entry (early finish, ls2_leave)
-    __threadfence();
+    // the workgroup's count, added by wave 0 before it leaves the entry (early finish, ls2_leave):
+    // one atomic and no fence per wave
+    if (lane == 0) s_done[wv] = done;
     __syncthreads();
-    if (wv == 0 && lane == 0) ls2_leave(st, mb, c.slot, c.gen);
+    if (wv == 0) {
+      uint32_t sum = lane < kLsWaves ? s_done[lane] : 0u;
+#pragma unroll
+      for (int m = kLsWaves / 2; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
+      if (lane == 0) {
+        if (sum) atomicAdd(&st->done[c.slot][(g % kPoolDoneShards) * 8], (unsigned long long)sum);
+        ls2_leave(st, mb, c.slot, c.gen);
+      }
+    }
     if (it >= iters || end) break;
     if (wv == 0) {
       const uint32_t next = ls2_pick(tab, st, mb, e, false);
