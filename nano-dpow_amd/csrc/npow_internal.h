@@ -138,14 +138,19 @@ static_assert(sizeof(PoolTableArg) + 2 * sizeof(void*) <= 4096, "kernel argument
 
 struct PoolSlotWord {
   unsigned long long dead;  // highest generation known dead in this slot
-  // Two-group kernels: workgroups on the slot's entry (npow_pool_kernel_ls2*; joins and leaves
-  // balance within every launch, so it is 0 between launches).  Once the entry is dead, whoever
-  // sees it at 0 publishes the slot's final nonce count (PoolMailbox::fin).
+  uint8_t pad[56];
+};
+// Two-group kernels: workgroups on the slot's entry (npow_pool_kernel_ls2*; joins and leaves
+// balance within every launch, so it is 0 between launches).  Once the entry is dead, whoever sees
+// it at 0 publishes the slot's final nonce count (PoolMailbox::fin).  A line of its own: beside
+// `dead`, which every wave loads every iteration, each join / leave atomic evicted that line.
+struct PoolSlotCount {
   unsigned long long wgs;
-  uint8_t pad[48];
+  uint8_t pad[56];
 };
 struct PoolDevState {
   PoolSlotWord slot[kMaxSlots];
+  PoolSlotCount count[kMaxSlots];
   unsigned long long done[kMaxSlots][kPoolDoneShards * 8];  // nonces hashed, sharded over 64-B lines
 };
 

@@ -745,6 +745,41 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
   }
 }
 
+// Live in-kernel clock (PoolClk): the first wave of workgroups 0..kClkWaves-1 -- one per XCD,
+// workgroups are dealt to XCDs round-robin -- reads s_memtime after its first instruction and
+// both counters after its last; 2 scalar reads and one 24-byte store per 4,096 waves.
+__device__ __forceinline__ bool clk_wave() { return blockIdx.x < (unsigned)kClkWaves && threadIdx.x < 64; }
+__device__ __forceinline__ uint64_t clk_begin() { return clk_wave() ? __builtin_amdgcn_s_memtime() : 0; }
+// The two-group kernels keep the start in LDS: a register live across the whole kernel was spilled to
+// scratch by every wave (8 bytes per lane: ~4 MB written and read back per launch, in PMC).
+__shared__ uint64_t s_clk_start;
+__device__ __forceinline__ void clk_begin_lds() {
+  if (clk_wave() && threadIdx.x == 0) s_clk_start = __builtin_amdgcn_s_memtime();
+}
+__device__ __forceinline__ void clk_end_ls2(const PoolTable* tab, PoolMailbox* mb, uint64_t t_start, uint32_t wv) {
+  // wave 0 of workgroups 0..kClkWaves-1; the work-item id is not kept to the end (it was spilled)
+  if (wv != 0 || blockIdx.x >= (unsigned)kClkWaves) return;
+  const uint64_t c_end = __builtin_amdgcn_s_memtime();
+  const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+  if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0) {
+    PoolClk* r = &mb->clk[tab->ring & 3][blockIdx.x];
+    __hip_atomic_store(&r->cycles, c_end - s_clk_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->ref, t_end - t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->seq, tab->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+__device__ __forceinline__ void clk_end(const PoolTable* tab, PoolMailbox* mb, uint64_t t_start, uint64_t c_start) {
+  if (!clk_wave()) return;
+  const uint64_t c_end = __builtin_amdgcn_s_memtime();
+  const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    PoolClk* r = &mb->clk[tab->ring & 3][blockIdx.x];
+    __hip_atomic_store(&r->cycles, c_end - c_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->ref, t_end - t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->seq, tab->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // The two-workgroups-per-CU form (npow_pool_kernel_ls2*): the same protocol as pool_body_ls with
 // the register budget of 8 waves per SIMD (64 VGPRs, 80 SGPRs, of which the stream takes 38 for
 // the uniforms it loads itself).  The loop keeps only what every iteration needs in registers:
@@ -758,16 +793,25 @@ __device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, 
 // entry is over once its dead word holds its generation (a win, a kill relay, a yield); a joiner
 // that then finds it dead leaves at once without hashing.  Whoever sees wgs at 0 after seeing the
 // entry dead -- the last leaver, or the marker itself -- sums the slot's done shards and publishes
-// the total (PoolMailbox::fin).  All of it is sequentially consistent at agent scope: a workgroup
-// that joins after that wgs read also finds the entry dead, and every hashing workgroup's done
-// adds precede its leave, so every published total is the final one (and equal, if two publish).
-// The host then finishes the job at once.  (A compare-and-swap join was measured: 512 workgroups
+// the total (PoolMailbox::fin).  The protocol's operations are agent-scope atomics, performed at the
+// device's point of coherence, and each one completes before the next is issued (s_waitcnt), so
+// they are sequentially consistent among themselves: a workgroup that joins after that wgs read
+// also finds the entry dead, and every hashing workgroup's done add precedes its leave, so every
+// published total is the final one (and equal, if two publish).  The host then finishes the job at
+// once.  (Sequentially consistent C++ atomics would also order every other memory access: an L2
+// write-back and invalidate around each operation, which quadrupled the search kernel's fetches --
+// 12.3 MB per launch against 2.8.  A compare-and-swap join was measured too: 512 workgroups
 // retrying on one word at every launch start cost 40 % of throughput.)
+__device__ __forceinline__ void ls2_complete() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ bool ls2_over(PoolDevState* st, uint32_t slot, uint64_t gen) {
-  return __hip_atomic_load(&st->slot[slot].dead, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT) >= gen;
+  const bool over = __hip_atomic_load(&st->slot[slot].dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= gen;
+  ls2_complete();
+  return over;
 }
 __device__ __forceinline__ bool ls2_empty(PoolDevState* st, uint32_t slot) {
-  return __hip_atomic_load(&st->slot[slot].wgs, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT) == 0;
+  const bool empty = __hip_atomic_load(&st->count[slot].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+  ls2_complete();
+  return empty;
 }
 
 __device__ __forceinline__ void ls2_publish_fin(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
@@ -781,14 +825,17 @@ __device__ __forceinline__ void ls2_publish_fin(PoolDevState* st, PoolMailbox* m
 
 // Leave the entry (after the workgroup's done adds); the last one out of a dead entry publishes.
 __device__ __forceinline__ void ls2_leave(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
+  ls2_complete();  // the workgroup's done add first
   const unsigned long long old =
-      __hip_atomic_fetch_add(&st->slot[slot].wgs, ~0ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&st->count[slot].wgs, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ls2_complete();
   if (old == 1ull && ls2_over(st, slot, gen) && ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
 }
 
 // Join it unless it is over (then leave again at once, without hashing).
 __device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
-  __hip_atomic_fetch_add(&st->slot[slot].wgs, 1ull, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(&st->count[slot].wgs, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ls2_complete();
   if (!ls2_over(st, slot, gen)) return true;
   ls2_leave(st, mb, slot, gen);
   return false;
@@ -796,14 +843,15 @@ __device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint
 
 // Mark it dead (a win, a kill relay, a yield); with no workgroup on it, publish now.
 __device__ __forceinline__ void ls2_kill(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
-  __hip_atomic_fetch_max(&st->slot[slot].dead, (unsigned long long)gen, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_max(&st->slot[slot].dead, (unsigned long long)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  ls2_complete();
   if (ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
 }
 
 __device__ __forceinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
                                              uint64_t wn, uint64_t wv) {
-  if (__hip_atomic_fetch_max(&st->slot[slot].dead, (unsigned long long)gen, __ATOMIC_SEQ_CST,
-                             __HIP_MEMORY_SCOPE_AGENT) < gen) {  // first win
+  if (__hip_atomic_fetch_max(&st->slot[slot].dead, (unsigned long long)gen, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT) < gen) {  // first win (the result waits for it)
     PoolWin* pw = &mb->win[slot];
     __hip_atomic_store(&pw->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&pw->value, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -823,15 +871,25 @@ __device__ __forceinline__ ConstEntry* ls2_entry(const PoolTable* tab, const Poo
   const PoolEntry* p = e < tab->n ? &tab->e[e] : &mb->dyn[(tab->dyn_base + (e - tab->n)) % kDynEntries].e;
   return (ConstEntry*)(uintptr_t)p;
 }
+// Relaxed: an acquire at system scope invalidates the L2, which at every poll cost 4x the search
+// kernel's fetches.  But a ring position's lines may still sit in an XCD's L2 from an earlier launch
+// (measured: wrong uniforms, invalid work), so a workgroup acquires once after it first sees a newly
+// published entry (ls2_fresh; *seen is its LDS count of the entries it has acquired for).
 __device__ __forceinline__ uint64_t ls2_ctl(PoolMailbox* mb) {
-  return __hip_atomic_load(&mb->ctl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+  return __hip_atomic_load(&mb->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void ls2_fresh(uint32_t nd, uint32_t* seen) {
+  if (nd > *seen) {
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the host wrote the entries
+    *seen = nd;
+  }
 }
 __device__ __forceinline__ uint32_t ls2_dyn_count(const PoolTable* tab, uint64_t ctl) {
   const uint32_t d = (uint32_t)ctl - tab->dyn_base;
   return d < (uint32_t)kDynEntries ? d : (uint32_t)kDynEntries;
 }
 __device__ __forceinline__ unsigned long long ls2_wgs(PoolDevState* st, uint32_t slot) {
-  return __hip_atomic_load(&st->slot[slot].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(&st->count[slot].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // A polling wave (lane 0 only): the host words of the entry.  Returns true when the wave's
@@ -839,10 +897,12 @@ __device__ __forceinline__ unsigned long long ls2_wgs(PoolDevState* st, uint32_t
 // killed, or it is unbounded and a dynamic entry has at least two workgroups fewer than it (the
 // workgroup moves there: a job that joined the running launch collects its share a workgroup at a
 // time, each from the most crowded entry among the pollers).
-__device__ __forceinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e) {
+__device__ __forceinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
+                                         uint32_t* seen) {
   const ConstEntry* pe = ls2_entry(tab, mb, e);
   const uint64_t ctl = ls2_ctl(mb);
   const uint32_t nd = ls2_dyn_count(tab, ctl);
+  ls2_fresh(nd, seen);
   bool leave = false;
   if ((ctl >> 32) != (tab->yield_base >> 32)) {
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
@@ -871,8 +931,10 @@ __device__ __forceinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st,
 // live unbounded entry with the fewest workgroups, ties broken by a hash of the workgroup index so
 // that the workgroups leaving one entry spread over the others.  Each lane looks at one entry.
 __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
-                                          bool first) {
-  const uint32_t lane = threadIdx.x & 63, g = blockIdx.x;
+                                          bool first, uint32_t* seen) {
+  // the lane from mbcnt, not threadIdx: a callee that reads the work-item id makes every wave keep
+  // (and spill) the register the ABI passes it in
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)), g = blockIdx.x;
   if (first) {
     uint32_t ok = 0;
     if (lane == 0) {
@@ -881,7 +943,9 @@ __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st
     }
     if (__builtin_amdgcn_readfirstlane(ok)) return e;
   }
-  const uint32_t N = tab->n + ls2_dyn_count(tab, ls2_ctl(mb));  // <= kMaxSlots = 64: one lane each
+  const uint32_t nd = ls2_dyn_count(tab, ls2_ctl(mb));
+  const uint32_t N = tab->n + nd;  // <= kMaxSlots = 64: one lane each
+  ls2_fresh(nd, seen);
   for (int attempt = 0; attempt < 4; ++attempt) {
     unsigned long long key = ~0ull;
     if (lane < N && lane != e) {
@@ -915,6 +979,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   __shared__ uint32_t s_flag;     // lane 0 of a polling wave -> its wave: leave the entry
   __shared__ uint32_t s_next;
   __shared__ uint32_t s_done[kLsWaves];  // each wave's nonces on the entry it is leaving
+  __shared__ uint32_t s_seen;            // dynamic entries this workgroup has acquired for (ls2_fresh)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t g = blockIdx.x, G = gridDim.x;
@@ -922,7 +987,8 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   const uint32_t n = tab->n, iters = tab->iters;
   if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
   if (wv == 0) {
-    const uint32_t first = ls2_pick(tab, st, mb, g % n, true);  // its own entry first
+    if (lane == 0) s_seen = 0;
+    const uint32_t first = ls2_pick(tab, st, mb, g % n, true, &s_seen);  // its own entry first
     if (lane == 0) s_next = first;
   }
   __syncthreads();
@@ -964,10 +1030,16 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       if (__builtin_expect(hits != 0, 0)) {
         const int wl = __builtin_ctzll(hits);
         const uint64_t wn = readlane64(nonce, wl), wval = readlane64(value, wl);
-        if (lane == 0) ls2_publish_win(st, mb, c.slot, c.gen, wn, wval);
+        if (lane == 0) {
+          // the entry's slot and generation re-read from it (c.up points at the entry): kept live for
+          // this rare branch they were spilled to scratch by every wave at every entry it joined
+          ConstEntry* ce = (ConstEntry*)(uintptr_t)c.up;
+          asm volatile("" : "+s"(ce));
+          ls2_publish_win(st, mb, ce->slot, ce->gen, wn, wval);
+        }
       }
       if (__builtin_expect(((it0 + w) & poll_mask) == 0, 0)) {
-        if (lane == 0) s_flag = ls2_poll(tab, st, mb, e) ? 1u : 0u;  // the wave's own LDS word use:
+        if (lane == 0) s_flag = ls2_poll(tab, st, mb, e, &s_seen) ? 1u : 0u;  // the wave's own LDS word use:
         lds_drain();                                                 // no other wave touches s_flag
         leave = leave || __builtin_amdgcn_readfirstlane(
                              __hip_atomic_load(&s_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) != 0;
@@ -1008,7 +1080,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     }
     if (it >= iters || end) break;
     if (wv == 0) {
-      const uint32_t next = ls2_pick(tab, st, mb, e, false);
+      const uint32_t next = ls2_pick(tab, st, mb, e, false, &s_seen);
       if (lane == 0) {
         s_next = next;
         s_stop[(seg + 1) % 3] = ~0u;
@@ -1018,24 +1090,9 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     ++seg;
   }
+  clk_end_ls2(tab, mb, t_start, wv);
 }
 
-// Live in-kernel clock (PoolClk): the first wave of workgroups 0..kClkWaves-1 -- one per XCD,
-// workgroups are dealt to XCDs round-robin -- reads s_memtime after its first instruction and
-// both counters after its last; 2 scalar reads and one 24-byte store per 4,096 waves.
-__device__ __forceinline__ bool clk_wave() { return blockIdx.x < (unsigned)kClkWaves && threadIdx.x < 64; }
-__device__ __forceinline__ uint64_t clk_begin() { return clk_wave() ? __builtin_amdgcn_s_memtime() : 0; }
-__device__ __forceinline__ void clk_end(const PoolTable* tab, PoolMailbox* mb, uint64_t t_start, uint64_t c_start) {
-  if (!clk_wave()) return;
-  const uint64_t c_end = __builtin_amdgcn_s_memtime();
-  const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-  if (threadIdx.x == 0) {
-    PoolClk* r = &mb->clk[tab->ring & 3][blockIdx.x];
-    __hip_atomic_store(&r->cycles, c_end - c_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&r->ref, t_end - t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&r->seq, tab->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
 
 // The table in device memory (uploaded in stream order before the launch).
 template <bool BOUNDED>
@@ -1102,9 +1159,8 @@ __global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2(const PoolTa
                                                                    PoolMailbox* __restrict__ mb) {
   uint64_t t_start;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
-  const uint64_t c_start = clk_begin();
-  pool_body_ls2<BOUNDED>(tab, st, mb, t_start);
-  clk_end(tab, mb, t_start, c_start);
+  clk_begin_lds();
+  pool_body_ls2<BOUNDED>(tab, st, mb, t_start);  // records the clock at its end (clk_end_ls2)
 }
 
 template <bool BOUNDED>
@@ -1115,9 +1171,8 @@ __global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2_arg(const Po
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
   (void)targ;
   const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();
-  const uint64_t c_start = clk_begin();
-  pool_body_ls2<BOUNDED>(tab, st, mb, t_start);
-  clk_end(tab, mb, t_start, c_start);
+  clk_begin_lds();
+  pool_body_ls2<BOUNDED>(tab, st, mb, t_start);  // records the clock at its end (clk_end_ls2)
 }
 
 hipError_t launch_pool(const PoolShape& sh, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,

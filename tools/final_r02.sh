@@ -1,7 +1,8 @@
 #!/bin/bash
 # Round-2 closing measurements on one GPU box (every GPU step under its own time limit, the chain
 # stops at the first failure): GPU suite, smoke, the driver's bench command, the rocprofv3 kernel
-# trace of the timed region, PMC traffic of the search kernel, and every bench workload.
+# trace of the timed region, PMC traffic of the search kernel; with a second argument "workloads",
+# every bench workload too (tools/workloads_refresh.sh; run it as its own call: gpurun's limit).
 set -o pipefail
 TAG=${1:-r02f}
 mkdir -p gpurun_out
@@ -13,5 +14,5 @@ P="python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline --latency-searches 
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$TAG -o run -- $P > gpurun_out/bench_prof_$TAG.json 2> gpurun_out/prof_$TAG.err || exit 1
 python3 tools/rocprof_timed_region.py gpurun_out/prof_$TAG/run_kernel_trace.csv gpurun_out/bench_prof_$TAG.json npow_pool_kernel_ls2_arg "rocprofv3 --kernel-trace --stats -- $P" > gpurun_out/timed_region_$TAG.txt || exit 1
 bash tools/pmc_bench.sh $TAG npow_pool_kernel_ls2 gpurun_out/pmc_pool_$TAG.json -- --steps 100 --warmup 5 --latency-searches 0 || exit 1
-bash tools/workloads_refresh.sh $TAG || exit 1
+[ "$2" = "workloads" ] && { bash tools/workloads_refresh.sh $TAG || exit 1; }
 tail -2 gpurun_out/pytest_gpu_$TAG.log; cat gpurun_out/smoke_$TAG.log gpurun_out/timed_region_$TAG.txt
