@@ -141,16 +141,19 @@ struct PoolSlotWord {
   uint8_t pad[56];
 };
 // Two-group kernels: workgroups on the slot's entry (npow_pool_kernel_ls2*; joins and leaves
-// balance within every launch, so it is 0 between launches).  Once the entry is dead, whoever sees
-// it at 0 publishes the slot's final nonce count (PoolMailbox::fin).  A line of its own: beside
-// `dead`, which every wave loads every iteration, each join / leave atomic evicted that line.
+// balance within every launch, so they are 0 between launches), one counter per XCD shard
+// (workgroup index mod kWgsShards: 64 joins per word at a launch's start instead of 512).  Once the
+// entry is dead, whoever sees every shard at 0 publishes the slot's final nonce count
+// (PoolMailbox::fin).  Lines of their own: beside `dead`, which every wave loads every iteration,
+// each join / leave atomic would evict that line.
+constexpr int kWgsShards = 8;
 struct PoolSlotCount {
   unsigned long long wgs;
   uint8_t pad[56];
 };
 struct PoolDevState {
   PoolSlotWord slot[kMaxSlots];
-  PoolSlotCount count[kMaxSlots];
+  PoolSlotCount count[kMaxSlots][kWgsShards];
   unsigned long long done[kMaxSlots][kPoolDoneShards * 8];  // nonces hashed, sharded over 64-B lines
 };
 

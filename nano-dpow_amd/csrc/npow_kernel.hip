@@ -788,7 +788,7 @@ __device__ __forceinline__ void clk_end(const PoolTable* tab, PoolMailbox* mb, u
 //
 // Early finish: a won or killed entry usually shares its launch with live ones, which keep the
 // launch running for the rest of its budget; the job's nonce count would only be read back after
-// that.  Instead wave 0 of a workgroup joins an entry (adds 1 to the slot's wgs word) before its
+// that.  Instead wave 0 of a workgroup joins an entry (adds 1 to its shard of the slot's wgs counters) before its
 // waves hash it, and leaves it (subtracts 1) after all 16 waves have added their done counts.  An
 // entry is over once its dead word holds its generation (a win, a kill relay, a yield); a joiner
 // that then finds it dead leaves at once without hashing.  Whoever sees wgs at 0 after seeing the
@@ -808,11 +808,17 @@ __device__ __forceinline__ bool ls2_over(PoolDevState* st, uint32_t slot, uint64
   ls2_complete();
   return over;
 }
+// Every shard at 0, read one after another after the entry was seen dead: a shard read as 0 means a
+// later joiner on that shard will find the entry dead.
 __device__ __forceinline__ bool ls2_empty(PoolDevState* st, uint32_t slot) {
-  const bool empty = __hip_atomic_load(&st->count[slot].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-  ls2_complete();
-  return empty;
+  for (int k = 0; k < kWgsShards; ++k) {
+    const bool zero = __hip_atomic_load(&st->count[slot][k].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+    ls2_complete();
+    if (!zero) return false;
+  }
+  return true;
 }
+__device__ __forceinline__ uint32_t ls2_shard() { return blockIdx.x % kWgsShards; }
 
 __device__ __forceinline__ void ls2_publish_fin(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
   unsigned long long total = 0;
@@ -827,18 +833,51 @@ __device__ __forceinline__ void ls2_publish_fin(PoolDevState* st, PoolMailbox* m
 __device__ __forceinline__ void ls2_leave(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
   ls2_complete();  // the workgroup's done add first
   const unsigned long long old =
-      __hip_atomic_fetch_add(&st->count[slot].wgs, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(&st->count[slot][ls2_shard()].wgs, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   ls2_complete();
   if (old == 1ull && ls2_over(st, slot, gen) && ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
 }
 
 // Join it unless it is over (then leave again at once, without hashing).
 __device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
-  __hip_atomic_fetch_add(&st->count[slot].wgs, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_fetch_add(&st->count[slot][ls2_shard()].wgs, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   ls2_complete();
   if (!ls2_over(st, slot, gen)) return true;
   ls2_leave(st, mb, slot, gen);
   return false;
+}
+
+// The same leave by all 64 lanes of wave 0, with the workgroup's count: the checks and the sum of the
+// done shards load in parallel (one lane per shard) instead of ~40 round trips one after another --
+// the last leaver's publish is on the path of a won job's reply.
+__device__ __forceinline__ void ls2_leave_wave(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
+                                               uint32_t sum) {
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  unsigned long long old = 0;
+  if (lane == 0) {
+    if (sum) atomicAdd(&st->done[slot][(blockIdx.x % kPoolDoneShards) * 8], (unsigned long long)sum);
+    ls2_complete();  // the count first
+    old = __hip_atomic_fetch_add(&st->count[slot][ls2_shard()].wgs, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ls2_complete();
+  }
+  if (__builtin_amdgcn_readfirstlane((uint32_t)old) != 1u || (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(old >> 32)) != 0u)
+    return;
+  const bool over = load_dead(st, slot) >= gen;  // every lane, same word
+  ls2_complete();
+  if (!__builtin_amdgcn_readfirstlane(over ? 1u : 0u)) return;
+  const bool busy = lane < kWgsShards &&
+                    __hip_atomic_load(&st->count[slot][lane].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+  ls2_complete();
+  if (__ballot(busy) != 0) return;
+  unsigned long long t = lane < kPoolDoneShards
+                             ? __hip_atomic_load(&st->done[slot][lane * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                             : 0ull;
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+  if (lane == 0) {
+    __hip_atomic_store(&mb->fin[slot].total, (uint64_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mb->fin[slot].gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // Mark it dead (a win, a kill relay, a yield); with no workgroup on it, publish now.
@@ -888,8 +927,10 @@ __device__ __forceinline__ uint32_t ls2_dyn_count(const PoolTable* tab, uint64_t
   const uint32_t d = (uint32_t)ctl - tab->dyn_base;
   return d < (uint32_t)kDynEntries ? d : (uint32_t)kDynEntries;
 }
+// Occupancy for balancing: this XCD shard's workgroups on the entry (workgroups are dealt to the XCDs
+// round-robin, so balancing each shard balances the whole).
 __device__ __forceinline__ unsigned long long ls2_wgs(PoolDevState* st, uint32_t slot) {
-  return __hip_atomic_load(&st->count[slot].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return __hip_atomic_load(&st->count[slot][ls2_shard()].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // A polling wave (lane 0 only): the host words of the entry.  Returns true when the wave's
@@ -939,7 +980,7 @@ __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st
     uint32_t ok = 0;
     if (lane == 0) {
       ConstEntry* pe = ls2_entry(tab, mb, e);
-      ok = load_dead(st, pe->slot) < pe->gen && ls2_join(st, mb, pe->slot, pe->gen) ? 1u : 0u;
+      ok = ls2_join(st, mb, pe->slot, pe->gen) ? 1u : 0u;  // (the join checks dead itself)
     }
     if (__builtin_amdgcn_readfirstlane(ok)) return e;
   }
@@ -1073,10 +1114,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       uint32_t sum = lane < kLsWaves ? s_done[lane] : 0u;
 #pragma unroll
       for (int m = kLsWaves / 2; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
-      if (lane == 0) {
-        if (sum) atomicAdd(&st->done[c.slot][(g % kPoolDoneShards) * 8], (unsigned long long)sum);
-        ls2_leave(st, mb, c.slot, c.gen);
-      }
+      ls2_leave_wave(st, mb, c.slot, c.gen, sum);
     }
     if (it >= iters || end) break;
     if (wv == 0) {

@@ -613,10 +613,15 @@ int Worker::launch() {
   // The second launch in flight only has to be queued before the running one ends (its budget
   // is known): queued early, it would sit behind a launch that a win ends, and the job could
   // only be retired after it too had started and drained (~20 us of every search's latency).
+  // ... unless no live entry is left in it (its jobs won or were killed: it ends within a hash, and a
+  // job finished early returns before that) -- then the next launch queues behind it at once.
   if (q_.size() == 1 && g_budget_us.load() > 0 &&
       std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - front_start_).count() <
-          (double)g_budget_us.load() - kPrelaunchUs)
-    return NPOW_OK;
+          (double)g_budget_us.load() - kPrelaunchUs) {
+    bool live = false;
+    for (int k = 0; k < kMaxSlots && !live; ++k) live = slots_[k].state == SlotState::kActive && !slots_[k].fresh;
+    if (live) return NPOW_OK;
+  }
   const PoolShape sh = pool_shape(d_);
   const uint32_t iters = sh.launch_iters(g_iters.load());
   PoolTable& t = *d_.h_tab[ring_];
