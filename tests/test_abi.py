@@ -74,3 +74,19 @@ def test_init_without_gpu_reports_no_device():
     assert rc == _lib.NPOW_ERR_NO_DEVICE
     with pytest.raises(_lib.NanoPowError):
         _lib.Engine()
+
+
+def test_device_stats_layout_matches_header(tmp_path):
+    """The ctypes mirror of npow_device_stats (_lib.DeviceStats) has the C struct's size and field
+    offsets: compiled from include/nanopow.h with gcc and compared field by field."""
+    fields = [f for f, _ in _lib.DeviceStats._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "nanopow.h"\nint main(void) {\n'
+                   '  printf("%zu\\n", sizeof(npow_device_stats));\n'
+                   + "".join(f'  printf("%zu\\n", offsetof(npow_device_stats, {f}));\n' for f in fields)
+                   + "  return 0;\n}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(_lib.DeviceStats)
+    assert vals[1:] == [getattr(_lib.DeviceStats, f).offset for f in fields]
