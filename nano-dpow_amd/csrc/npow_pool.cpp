@@ -14,9 +14,16 @@
 // kMaxSlots roots live in every launch, so a root that is won mid-launch costs nothing:
 // its waves move on to the other live roots (npow_kernel.hip, npow_pool_kernel).
 //
+// With the two-group kernel (the default) a job also leaves its launch early in both directions:
+// a won or killed job finishes from the final nonce count the kernel publishes once no workgroup is
+// left on its entry (early_finish; PoolMailbox::fin), and a new unbounded job joins the running
+// launch as a dynamic entry (dyn_add; PoolMailbox::dyn) instead of ending it (yield_if_long, now
+// the fallback).  DESIGN.md section 1.
+//
 // Threads: one persistent worker per device (started by npow_init) owns the device's
 // stream, its slot table and up to two launches in flight (the second is queued only near
-// the end of the first one's budget); callers block in pool_wait.  The
+// the end of the first one's budget, or at once behind a launch with no live entry left);
+// callers block in pool_wait.  The
 // only cross-device datum is a job's outcome: the first device whose winner passes CPU
 // re-validation decides the job, the others raise their slot's kill word (pinned host
 // memory that the waves poll) and retire it.  No collective, no device-to-device traffic.
