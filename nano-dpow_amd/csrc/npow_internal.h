@@ -121,7 +121,10 @@ struct PoolTable {
   uint32_t seq;           // ... tagged with the launch's sequence number (low 32 bits)
   uint32_t dyn_base;      // two-group kernels: the low half of PoolMailbox::ctl when the table was built -- the
                           // launch may also search the entries the host publishes after it
-  uint32_t pad[7];
+  uint32_t counted;       // two-group kernels: workgroups are counted on their entries (early finish,
+                          // dynamic entries).  The host sets it for tables of 2 or more entries: a
+                          // launch with one entry ends with it, and counting only slows its end.
+  uint32_t pad[6];
   PoolEntry e[kMaxSlots];
 };
 inline size_t pool_table_bytes(uint32_t n) { return offsetof(PoolTable, e) + (size_t)n * sizeof(PoolEntry); }

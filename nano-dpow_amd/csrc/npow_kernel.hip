@@ -838,8 +838,10 @@ __device__ __forceinline__ void ls2_leave(PoolDevState* st, PoolMailbox* mb, uin
   if (old == 1ull && ls2_over(st, slot, gen) && ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
 }
 
-// Join it unless it is over (then leave again at once, without hashing).
-__device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
+// Join it unless it is over (then leave again at once, without hashing).  Uncounted launches
+// (PoolTable::counted) only check that it is live.
+__device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen, bool counted) {
+  if (!counted) return load_dead(st, slot) < gen;
   __hip_atomic_fetch_add(&st->count[slot][ls2_shard()].wgs, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   ls2_complete();
   if (!ls2_over(st, slot, gen)) return true;
@@ -851,9 +853,13 @@ __device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint
 // done shards load in parallel (one lane per shard) instead of ~40 round trips one after another --
 // the last leaver's publish is on the path of a won job's reply.
 __device__ __forceinline__ void ls2_leave_wave(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
-                                               uint32_t sum) {
+                                               uint32_t sum, bool counted) {
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   unsigned long long old = 0;
+  if (!counted) {
+    if (lane == 0 && sum) atomicAdd(&st->done[slot][(blockIdx.x % kPoolDoneShards) * 8], (unsigned long long)sum);
+    return;
+  }
   if (lane == 0) {
     if (sum) atomicAdd(&st->done[slot][(blockIdx.x % kPoolDoneShards) * 8], (unsigned long long)sum);
     ls2_complete();  // the count first
@@ -881,10 +887,10 @@ __device__ __forceinline__ void ls2_leave_wave(PoolDevState* st, PoolMailbox* mb
 }
 
 // Mark it dead (a win, a kill relay, a yield); with no workgroup on it, publish now.
-__device__ __forceinline__ void ls2_kill(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
+__device__ __forceinline__ void ls2_kill(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen, bool counted) {
   __hip_atomic_fetch_max(&st->slot[slot].dead, (unsigned long long)gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   ls2_complete();
-  if (ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
+  if (counted && ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
 }
 
 __device__ __forceinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
@@ -948,12 +954,12 @@ __device__ __forceinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st,
   if ((ctl >> 32) != (tab->yield_base >> 32)) {
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
       ConstEntry* q = ls2_entry(tab, mb, k);
-      if (!q->bounded) ls2_kill(st, mb, q->slot, q->gen);
+      if (!q->bounded) ls2_kill(st, mb, q->slot, q->gen, tab->counted != 0);
     }
     leave = !pe->bounded;
   }
   if (__hip_atomic_load(&mb->kill[pe->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == pe->gen) {
-    ls2_kill(st, mb, pe->slot, pe->gen);  // relay
+    ls2_kill(st, mb, pe->slot, pe->gen, tab->counted != 0);  // relay
     leave = true;
   }
   if (!leave && !pe->bounded && nd > 0) {
@@ -980,7 +986,7 @@ __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st
     uint32_t ok = 0;
     if (lane == 0) {
       ConstEntry* pe = ls2_entry(tab, mb, e);
-      ok = ls2_join(st, mb, pe->slot, pe->gen) ? 1u : 0u;  // (the join checks dead itself)
+      ok = ls2_join(st, mb, pe->slot, pe->gen, tab->counted != 0) ? 1u : 0u;  // (the join checks dead itself)
     }
     if (__builtin_amdgcn_readfirstlane(ok)) return e;
   }
@@ -1006,7 +1012,7 @@ __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st
     uint32_t ok = 0;
     if (lane == 0) {
       ConstEntry* q = ls2_entry(tab, mb, pick);
-      ok = ls2_join(st, mb, q->slot, q->gen) ? 1u : 0u;
+      ok = ls2_join(st, mb, q->slot, q->gen, tab->counted != 0) ? 1u : 0u;
     }
     if (__builtin_amdgcn_readfirstlane(ok)) return pick;
   }
@@ -1114,7 +1120,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       uint32_t sum = lane < kLsWaves ? s_done[lane] : 0u;
 #pragma unroll
       for (int m = kLsWaves / 2; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
-      ls2_leave_wave(st, mb, c.slot, c.gen, sum);
+      ls2_leave_wave(st, mb, c.slot, c.gen, sum, tab->counted != 0);
     }
     if (it >= iters || end) break;
     if (wv == 0) {

@@ -285,6 +285,7 @@ struct PoolInflight {
   int ring;
   uint64_t dyn_base;    // PoolTable::dyn_base of the launch
   uint64_t yield_base;  // PoolTable::yield_base of the launch
+  bool counted;         // PoolTable::counted: early finish and dynamic entries are on in it
 };
 
 class Worker {
@@ -406,6 +407,7 @@ bool Worker::dyn_add(int s) {
   const PoolShape sh = pool_shape(d_);
   if (!sh.lockstep || sh.groups != 2) return false;
   const PoolInflight& f = q_.front();
+  if (!f.counted) return false;  // a one-entry launch: the new job ends it (a yield) instead
   if ((uint32_t)((uint32_t)ctl_ - (uint32_t)f.dyn_base) >= (uint32_t)kDynEntries) return false;
   if ((ctl_ >> 32) != (f.yield_base >> 32)) return false;  // it is ending
   bool other = false;  // another live entry keeps the launch running (workgroups to move)
@@ -644,6 +646,10 @@ int Worker::launch() {
   t.budget = g_budget_us.load() * 100u;  // s_memrealtime runs at 100 MHz
   t.yield_base = ctl_;
   t.dyn_base = (uint32_t)ctl_;
+  // One entry: the launch ends with it, and counting workgroups on it only delays that end (the
+  // final count would reach the host ~60 us after the launch's own end; measured with
+  // NANOPOW_TRACE_LATENCY).  Two or more: a won entry's job need not wait for the others.
+  t.counted = n >= 2 ? 1u : 0u;
   ++seq_;
   t.ring = (uint32_t)ring_;
   t.seq = (uint32_t)seq_;
@@ -704,7 +710,7 @@ int Worker::launch() {
   NPOW_DBG("nanopow[%d]: launch %llu n=%u slots:", d_.id, (unsigned long long)seq_, n);
   for (uint32_t e = 0; e < n; ++e) NPOW_DBG(" %d/g%llu", idx[e], (unsigned long long)t.e[e].gen);
   NPOW_DBG("\n");
-  q_.push_back({seq_, r, (uint32_t)ctl_, t.yield_base});
+  q_.push_back({seq_, r, (uint32_t)ctl_, t.yield_base, t.counted != 0});
   return NPOW_OK;
 }
 

@@ -202,35 +202,62 @@ def test_full_table_of_64_bounded_and_unbounded(gpu_engine):
 def test_new_job_does_not_wait_for_a_long_launch(gpu_engine):
     """With a 200-ms launch budget, a job submitted while another job's launch is running is
     searched within a few ms: the worker bumps the yield word, the running launch hands its
-    unbounded job back (re-adopted with a new generation), and the next launch holds both.  Once
-    it wins it returns at once (two-group kernels): its workgroups move to the busy job and the
-    last one to leave publishes the won entry's final count, so the job does not wait for the
-    launch the busy job keeps running (up to its iteration cap, ~65 ms here)."""
+    unbounded job back (re-adopted with a new generation), and the next launch holds both."""
     gpu_engine.set_pool_tuning(budget_us=200_000)
-    early = gpu_engine.pool_kernel_groups() == 2
     gpu_engine.reset_stats(0)
     try:
         tok = _lib.CancelToken()
         busy = gpu_engine.submit(bytes(range(32)), M64, device_mask=1, cancel=tok)
         time.sleep(0.05)  # the busy job's first 200-ms launch is running
         lat = []
+        for r in _roots(18, 5):
+            t0 = time.perf_counter()
+            res = gpu_engine.submit(r, RECEIVE, device_mask=1).wait(10)
+            lat.append(time.perf_counter() - t0)
+            assert res.status == _lib.NPOW_OK and oracle.work_value(r, res.nonce) == res.value >= RECEIVE
+        assert max(lat) < 0.1, lat
+        assert busy.wait(0) is None  # still searching after being handed back
+        tok.set()
+        res = busy.wait(10)
+        assert res.status == _lib.NPOW_CANCELLED and res.nonces_done > 0
+    finally:
+        gpu_engine.set_pool_tuning(budget_us=20_000)
+
+
+def test_new_jobs_join_a_running_launch_and_finish_early(gpu_engine):
+    """Two-group kernels, a launch of 2+ entries (counted): 8 receive-difficulty jobs submitted one
+    after another beside two busy jobs in 200-ms launches each join the running launch as a dynamic
+    entry (no yield) and return as soon as their entry's last workgroup has left it (early finish),
+    not when the busy jobs' launch ends (its iteration cap, ~65 ms here); every count the kernel
+    published equals the read-back after the launch, and all nonces add up to the device's counter."""
+    if gpu_engine.pool_kernel_groups() != 2:
+        pytest.skip("early finish and dynamic entries are two-group-kernel features")
+    gpu_engine.set_pool_tuning(budget_us=200_000)
+    gpu_engine.reset_stats(0)
+    try:
+        toks = [_lib.CancelToken() for _ in range(2)]
+        busy = [gpu_engine.submit(r, M64, device_mask=1, cancel=c) for r, c in zip(_roots(19, 2), toks)]
+        time.sleep(0.05)  # their launch (2 entries: counted) is running
+        lat, done = [], 0
         for r in _roots(18, 8):
             t0 = time.perf_counter()
             res = gpu_engine.submit(r, RECEIVE, device_mask=1).wait(10)
             lat.append(time.perf_counter() - t0)
             assert res.status == _lib.NPOW_OK and oracle.work_value(r, res.nonce) == res.value >= RECEIVE
-        assert max(lat) < (0.03 if early else 0.1), lat
-        if early:
-            assert sorted(lat)[len(lat) // 2] < 0.01, lat
-            st = gpu_engine.stats(0)
-            assert st.early_finishes >= len(lat) and st.early_mismatches == 0
-            # each new job joined the busy job's running launch as a dynamic entry: no launch ended
-            # early for it (the first launch may have been too close to its end to take one)
-            assert st.dyn_entries >= len(lat) - 1 and st.yields <= 1, (st.dyn_entries, st.yields)
-        assert busy.wait(0) is None  # still searching after being handed back
-        tok.set()
-        res = busy.wait(10)
-        assert res.status == _lib.NPOW_CANCELLED and res.nonces_done > 0
+            done += res.nonces_done
+        assert max(lat) < 0.03 and sorted(lat)[len(lat) // 2] < 0.01, lat
+        for c in toks:
+            c.set()
+        for t in busy:
+            res = t.wait(10)
+            assert res.status == _lib.NPOW_CANCELLED and res.nonces_done > 0
+            done += res.nonces_done
+        st = gpu_engine.stats(0)
+        # (the busy pair's first launch held only the first of them: the second ended it, and a
+        # receive job may have arrived before their two-entry launch started)
+        assert st.dyn_entries >= len(lat) - 1 and st.yields <= 2, (st.dyn_entries, st.yields)
+        assert st.early_finishes >= len(lat) and st.early_mismatches == 0, (st.early_finishes, st.early_mismatches)
+        assert st.nonces == done
     finally:
         gpu_engine.set_pool_tuning(budget_us=20_000)
 
