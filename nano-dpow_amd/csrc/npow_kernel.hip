@@ -1033,9 +1033,19 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   const uint32_t w = g * kLsWaves + wv;
   const uint32_t n = tab->n, iters = tab->iters;
   if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
+  const bool counted = tab->counted != 0;
   if (wv == 0) {
     if (lane == 0) s_seen = 0;
-    const uint32_t first = ls2_pick(tab, st, mb, g % n, true, &s_seen);  // its own entry first
+    // its own entry first.  An uncounted (one-entry) launch only checks that it is live: it may follow
+    // a counted launch that held the same entry and has published its final count, after which no
+    // nonce may be hashed for it (tests/test_gpu_configs.py caught one launch doing so).
+    uint32_t first;
+    if (counted) {
+      first = ls2_pick(tab, st, mb, g % n, true, &s_seen);
+    } else {
+      ConstEntry* pe = ls2_entry(tab, mb, g % n);
+      first = load_dead(st, pe->slot) < pe->gen ? g % n : kNoEntry;
+    }
     if (lane == 0) s_next = first;
   }
   __syncthreads();
@@ -1120,9 +1130,9 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       uint32_t sum = lane < kLsWaves ? s_done[lane] : 0u;
 #pragma unroll
       for (int m = kLsWaves / 2; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
-      ls2_leave_wave(st, mb, c.slot, c.gen, sum, tab->counted != 0);
+      ls2_leave_wave(st, mb, c.slot, c.gen, sum, counted);
     }
-    if (it >= iters || end) break;
+    if (it >= iters || end || !counted) break;  // an uncounted launch has no other entry
     if (wv == 0) {
       const uint32_t next = ls2_pick(tab, st, mb, e, false, &s_seen);
       if (lane == 0) {
