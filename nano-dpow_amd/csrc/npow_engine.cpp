@@ -318,6 +318,7 @@ int npow_init(int* n_devices) try {
   if (const char* l = getenv("NANOPOW_LS_LDS")) g_ls_lds = (uint32_t)atoi(l);
   if (const char* k = getenv("NANOPOW_LS_GROUPS")) g_ls_groups = atoi(k) == 1 ? 1 : 2;
   if (const char* b = getenv("NANOPOW_BUDGET_US")) g_budget_us = (uint32_t)atoi(b);  // A/B runs
+  if (const char* p = getenv("NANOPOW_POLL")) g_poll = (uint32_t)atoi(p);             // A/B runs
   int n_logical = n;
   if (const char* v = getenv("NANOPOW_VIRTUAL_DEVICES")) {
     const int k = atoi(v);
