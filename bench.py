@@ -16,12 +16,21 @@ rank 0 times --latency-searches (default 1,000) more searches on R_0..R_999 at
 the C ABI for a real p50 / p99 of time-to-work (ttw_c_abi_ms), and 100
 work_generate requests over one keep-alive HTTP connection (http_ttw_ms).
 
-Multi-GPU (``torch.distributed.run``, one rank per GPU): every rank searches
-its own roots on its own GPU (disjoint work, no data-path collective); gloo on
-the CPU carries only the barrier and the max/sum of the timings.
-Scaling is therefore "weak" (fixed searches per GPU).
+Multi-GPU, two ways (``--gpus N``):
+  * under ``torch.distributed.run`` (WORLD_SIZE = N, the driver's scaling runs): one rank per GPU,
+    every rank searching its own roots on its own GPU (disjoint work, no data-path collective);
+    gloo on the CPU carries only the barrier and the max/sum of the timings.  A rank that already
+    sees exactly one device (a launcher narrowed HIP_/CUDA_/ROCR_VISIBLE_DEVICES) keeps it; otherwise
+    it takes the LOCAL_RANK-th visible device.  Afterwards every rank searches the same roots on
+    disjoint strides, the first win cancelling the others through a shared word (node_ttw_ms);
+  * in one process (WORLD_SIZE unset, N > 1): the product's own multi-GPU path -- the work pool
+    over device_mask = N devices, N searches in flight, each split into N disjoint strides with
+    first-found cancellation across the GPUs (npow_pool.cpp); afterwards one root at a time over
+    all N (node_ttw_ms, with each search's overshoot: how long the other GPUs kept hashing after the
+    host accepted the winner).  Fails if fewer than N devices are visible.
+Scaling is "weak" either way (K searches per GPU).
 
-roofline: the dominant kernel (npow_pool_kernel<false>) is int32-VALU bound.
+roofline: the dominant kernel (npow_pool_kernel_ls2_arg<false>) is int32-VALU bound.
 achieved = nonces hashed in kernel x 2232 int32 ops/nonce /
 kernel time, the kernel time measured by HIP events recorded on the stream the
 kernel runs on (libnanopow stats); peak = 256 CUs x 128 int32 lanes/clk
@@ -69,49 +78,79 @@ import time
 HERE = os.path.dirname(os.path.abspath(__file__))
 WORLD = int(os.environ.get("WORLD_SIZE", "1"))
 LOCAL_RANK = int(os.environ.get("LOCAL_RANK", "0"))
+
+
+def _ids(v):
+    return [x.strip() for x in v.split(",") if x.strip()]
+
+
+def rank_visibility(env, local_rank: int):
+    """One GPU per rank under torch.distributed.run: the environment change (or None) that leaves
+    the rank exactly one visible device, or raises SystemExit if it cannot.  HIP enumerates the
+    devices ROCR_VISIBLE_DEVICES exposes, then applies HIP_VISIBLE_DEVICES (or, if that is unset,
+    CUDA_VISIBLE_DEVICES) as indices into them.  A rank that already sees exactly one device -- a
+    launcher narrowed one of the lists for it -- keeps it; a list of several is indexed by
+    LOCAL_RANK; with none set the rank takes device LOCAL_RANK."""
+    def get(k):  # an empty list is what a GPU-less container exports: as if unset
+        v = env.get(k)
+        return v if v is not None and v.strip() else None
+    hip, cuda, rocr = get("HIP_VISIBLE_DEVICES"), get("CUDA_VISIBLE_DEVICES"), get("ROCR_VISIBLE_DEVICES")
+    lst = hip if hip is not None else cuda
+    if lst is not None:
+        ids = _ids(lst)
+        if len(ids) == 1:
+            return None
+        if local_rank >= len(ids):
+            raise SystemExit(f"bench.py: LOCAL_RANK {local_rank} but only {len(ids)} visible devices "
+                             f"({'HIP' if hip is not None else 'CUDA'}_VISIBLE_DEVICES={lst!r})")
+        return {"HIP_VISIBLE_DEVICES": ids[local_rank]}
+    if rocr is not None:
+        ids = _ids(rocr)
+        if len(ids) == 1:
+            return None
+        if local_rank >= len(ids):
+            raise SystemExit(f"bench.py: LOCAL_RANK {local_rank} but ROCR_VISIBLE_DEVICES={rocr!r}")
+    return {"HIP_VISIBLE_DEVICES": str(local_rank)}
+
+
 if WORLD > 1:
-    # one GPU per rank: the engine of rank r sees only GPU LOCAL_RANK (as device 0).  A launcher
-    # that already exported a device list keeps its list; the rank takes its LOCAL_RANK-th entry.
-    _vis = os.environ.get("HIP_VISIBLE_DEVICES")
-    if _vis is None:
-        os.environ["HIP_VISIBLE_DEVICES"] = str(LOCAL_RANK)
-    elif "," in _vis:
-        _ids = [x for x in _vis.split(",") if x.strip()]
-        os.environ["HIP_VISIBLE_DEVICES"] = _ids[LOCAL_RANK % len(_ids)]
+    os.environ.update(rank_visibility(os.environ, LOCAL_RANK) or {})
 sys.path.insert(0, os.path.join(HERE, "nano-dpow_amd"))
 
 SEND = 0xfffffff800000000
 OPS_PER_NONCE = 2232                # SURVEY.md §8(d): int32 VALU ops of one 12-round compression
 PEAK_TOPS = 256 * 128 * 2.4e9 / 1e12  # MI355X: 256 CU x (4 SIMD x 32 lanes) x 2.4 GHz = 78.6 Tops/s
-# The generated stream's cost in a tail-free harness (informational, next to the roofline), per
-# search kernel (NANOPOW_POOL_KERNEL / NANOPOW_LS_GROUPS select the kernel at npow_init):
-#  * lockstep2 (default): two 1,024-lane workgroups per CU, the stream loading its own uniforms
-#    (1,677 VALU instructions): 4,852 SIMD cycles per wave-hash (64 nonces) in
-#    tools/experiments/stream_lockstep.py (profiles/r02_stream_bound_g2.jsonl "vop2_ld");
-#  * lockstep (NANOPOW_LS_GROUPS=1): one workgroup per CU, 5,042 cycles (r02_stream_bound_g1.jsonl);
-#  * seq (NANOPOW_POOL_KERNEL=seq): 1,671 instructions at 5,725 cycles, time-budgeted, every SIMD
-#    saturated (tools/valu_mix2.py "real hash stream": profiles/r01_valu_mix2_final_stream.jsonl).
-# The harness is not a strict bound: its workgroups start together and stay in step, while a
-# kernel's two groups per CU drift apart and overlap better (the kernel's own cycles per hash, from
-# its in-kernel clock, are reported beside it).
-POOL_KERNEL = ("seq" if os.environ.get("NANOPOW_POOL_KERNEL") == "seq" else
-               "lockstep" if os.environ.get("NANOPOW_LS_GROUPS") == "1" else "lockstep2")
-STREAM = {"lockstep2": {"cycles": 4852, "valu": 1677, "kernel": "npow_pool_kernel_ls2_arg<false>",
-                        "sweep_kernel": "npow_sweep_kernel_ls2",
-                        "src": "tools/experiments/stream_lockstep.py, profiles/r02_stream_bound_g2.jsonl"},
-          "lockstep": {"cycles": 5042, "valu": 1677, "kernel": "npow_pool_kernel_ls_arg<false>",
-                       "sweep_kernel": "npow_sweep_kernel_ls",
-                       "src": "tools/experiments/stream_lockstep.py, profiles/r02_stream_bound_g1.jsonl"},
-          "seq": {"cycles": 5725, "valu": 1671, "kernel": "npow_pool_kernel_arg<false>",
-                  "sweep_kernel": "npow_task_kernel<Mode::kSweep>",
-                  "src": "tools/valu_mix2.py, profiles/r01_valu_mix2_final_stream.jsonl"}}[POOL_KERNEL]
+STREAM_INC = os.path.join(HERE, "nano-dpow_amd", "csrc", "npow_hash_asm_lockstep_ld.inc")
+
+
+def stream_mix(path=STREAM_INC):
+    """The shipped stream's instruction mix, from the generator's header line of the committed file:
+    {opcode: count per nonce}, its VALU total, and the int32 ops it executes per nonce
+    (v_lshl_add_u64 = one 64-bit add = 2 ops; xor, alignbit, shift 1 each; v_mov 0)."""
+    import re
+    with open(path) as f:
+        head = f.read(2000)
+    m = re.search(r"Per nonce: (\d+) VALU instructions \(([^)]*)\)", head)
+    mix = {k: int(v) for k, v in (x.strip().rsplit(" ", 1) for x in m.group(2).split(","))}
+    ops = sum(2 * c if op == "v_lshl_add_u64" else (0 if op.startswith("v_mov") else c) for op, c in mix.items())
+    return {"valu": int(m.group(1)), "mix": mix, "executed_int32_ops": ops}
+
+
+# The generated stream's cost in a tail-free harness (informational, next to the roofline): two
+# 1,024-lane workgroups per CU, the stream loading its own uniforms (1,677 VALU instructions):
+# 4,852 SIMD cycles per wave-hash (64 nonces) in tools/experiments/stream_lockstep.py
+# (profiles/r02_stream_bound_g2.jsonl "vop2_ld").  The harness is not a strict bound: its workgroups
+# start together and stay in step, while a kernel's two groups per CU drift apart and overlap
+# better (the kernel's own cycles per hash, from its in-kernel clock, are reported beside it).
+STREAM = {"cycles": 4852, "valu": 1677, "kernel": "npow_pool_kernel_ls2_arg<false>",
+          "sweep_kernel": "npow_sweep_kernel_ls2",
+          "src": "tools/experiments/stream_lockstep.py, profiles/r02_stream_bound_g2.jsonl"}
 STREAM_CYCLES_PER_HASH = STREAM["cycles"]
 STREAM_CLOCK_GHZ = 2.39   # in-kernel s_memtime / s_memrealtime under this load
 STREAM_BOUND_GNPS = 1024 * 64 * STREAM_CLOCK_GHZ / STREAM_CYCLES_PER_HASH  # 1,024 SIMDs
-PMC_POOL = {"lockstep2": "r02_ls2_pmc_pool.json", "lockstep": "r02_lockstep_pmc_pool.json",
-            "seq": "r02_pmc_pool.json"}[POOL_KERNEL]
-PMC_SWEEP = {"lockstep2": "r02_ls2_pmc_sweep.json", "lockstep": "r02_lockstep_pmc_sweep.json",
-             "seq": "r01_pmc_sweep.json"}[POOL_KERNEL]
+# rocprofv3 PMC passes of the bench's own command (tools/pmc_bench.sh), newest first
+PMC_POOL = ("r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
+PMC_SWEEP = ("r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
 METRIC = "Gnonce/s blake2b-64 per GPU & 8-GPU node; p50 time-to-work at fffffff8"
 
 
@@ -484,22 +523,46 @@ class SclkSampler:
                           f"{int(self.period * 1e3)} ms over the warmup and timed searches"}
 
 
-def _pmc_traffic(name=PMC_POOL):
-    """HBM bytes per launch of the workload's dominant kernel measured by rocprofv3 PMC passes
-    (tools/pmc_bench.sh on that workload; FETCH_SIZE doubled per the gfx950 correction).  PMC
-    needs the profiler around the process, so the bench reports the committed measurement;
-    None if absent."""
-    try:
-        with open(os.path.join(HERE, "profiles", name)) as f:
-            return json.load(f)["hbm_bytes_per_launch"]
-    except (OSError, ValueError, KeyError):
+def _pmc(names=PMC_POOL):
+    """(file name, contents) of the newest committed rocprofv3 PMC summary of the workload's dominant
+    kernel (tools/pmc_bench.sh on that workload; FETCH_SIZE doubled per the gfx950 correction).  PMC
+    needs the profiler around the process, so the bench reports the committed measurement; (None,
+    None) if absent."""
+    for name in names:
+        try:
+            with open(os.path.join(HERE, "profiles", name)) as f:
+                return name, json.load(f)
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
+def _pmc_traffic(names=PMC_POOL):
+    return (_pmc(names)[1] or {}).get("hbm_bytes_per_launch")
+
+
+def pmc_nonces_per_dispatch(pmc, valu_per_iteration):
+    """Nonces per dispatch implied by the PMC instruction count: SQ_INSTS_VALU per dispatch / the VALU
+    instructions of one wave iteration (the stream + the loop's own) x 64 lanes."""
+    if not pmc:
         return None
+    c = pmc.get("counters_mean", {})
+    if "SQ_INSTS_VALU" not in c:
+        return None
+    return c["SQ_INSTS_VALU"] / valu_per_iteration * 64
 
 
-def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, kern_nonces, launches):
+LOOP_VALU = 5  # the search loop's VALU instructions per iteration besides the stream (DESIGN.md section 4)
+
+
+def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, kern_nonces, launches, parallelism=None):
     gnps = tot_nonces / max_wall / 1e9
     per_rank_kernel_s = kern_ms * 1e-3 / world
     achieved = (kern_nonces / world) * OPS_PER_NONCE / per_rank_kernel_s / 1e12 if kern_ms > 0 else 0.0
+    mix = stream_mix()
+    ex = mix["executed_int32_ops"]
+    pmc_name, pmc = _pmc(PMC_POOL)
+    pmc_npd = pmc_nonces_per_dispatch(pmc, mix["valu"] + LOOP_VALU)
     return {
         "metric": METRIC,
         "value": round(gnps, 4),
@@ -519,9 +582,10 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
             "threshold": "fffffff800000000",
             "searches_per_gpu": steps,
             "searches_total": len(all_ttw),
-            "parallelism": f"dp{world} (disjoint roots per GPU, no collective)" if world == 1 else
-                           f"dp{world} ({len(all_ttw)} searches drawn from one node-wide queue by {world} "
-                           "one-GPU ranks; disjoint roots, no collective)",
+            "parallelism": parallelism or (
+                f"dp{world} (disjoint roots per GPU, no collective)" if world == 1 else
+                f"dp{world} ({len(all_ttw)} searches drawn from one node-wide queue by {world} "
+                "one-GPU ranks; disjoint roots, no collective)"),
         },
         "p50_ttw_ms": round(pct(all_ttw, 50) * 1e3, 3),
         # a p99 needs ~100 samples: fewer (the driver's 20 timed steps) report the maximum as such
@@ -537,19 +601,28 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
             "peak": round(PEAK_TOPS, 3),
             "unit": "Tops/s (int32 VALU)",
             "frac": round(achieved / PEAK_TOPS, 4),
-            "traffic": _pmc_traffic(),
+            "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
             "traffic_unit": "HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
-                            f"(profiles/{PMC_POOL}, "
-                            "tools/pmc_bench.sh); algorithmic bytes: 0",
+                            f"(profiles/{pmc_name}, tools/pmc_bench.sh); algorithmic bytes: 0",
             "ops_per_nonce": OPS_PER_NONCE,
+            "ops_note": "algorithmic int32 ops of one 12-round compression (SURVEY.md §8d); the stream executes "
+                        "fewer: host precompute of nonce-independent steps and round 12's dead half removed",
+            "executed_ops_per_nonce": ex,
+            "executed_mix": mix["mix"],
+            "frac_executed": round(achieved * ex / OPS_PER_NONCE / PEAK_TOPS, 4),
             "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
             "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
+            "nonces_per_launch": round(kern_nonces / launches) if launches else None,
+            "pmc_nonces_per_dispatch": round(pmc_npd) if pmc_npd else None,
+            "pmc_note": (f"profiles/{pmc_name}: SQ_INSTS_VALU per dispatch / ({mix['valu']} stream + {LOOP_VALU} "
+                         "loop VALU per wave iteration) x 64 lanes; that run's own launches (its avg_launch_ms "
+                         "and clock), to compare with nonces_per_launch") if pmc_npd else None,
             "launches": launches,
             "stream_harness": {
                 "gnps": round(STREAM_BOUND_GNPS, 3),
                 "cycles_per_hash": STREAM_CYCLES_PER_HASH,
                 "kernel_cycles_per_hash": None,  # filled in once the in-kernel clock is known (main)
-                "what": f"the {POOL_KERNEL} kernel's generated {STREAM['valu']:,}-instruction stream in a tail-free "
+                "what": f"the generated {STREAM['valu']:,}-instruction stream in a tail-free "
                         f"harness ({STREAM_CYCLES_PER_HASH:,} SIMD cycles per 64 nonces, i.e. {STREAM_BOUND_GNPS:.2f} "
                         f"Gnonce/s at {STREAM_CLOCK_GHZ} GHz; {STREAM['src']}); kernel_cycles_per_hash is the "
                         "kernel's own figure at its in-kernel clock; the roofline frac is capped by the stream's "
@@ -575,35 +648,25 @@ def _reduce(dist, nonces, wall, ttw, extra_sum=()):
 
 
 def workload_allgpus(eng, args, rank, world, dist):
-    """One process, every visible GPU on one root at a time (npow_search, device_mask 0)."""
+    """One process, --gpus GPUs (default every visible one) on one root at a time: config 2 at N GPUs."""
     if world > 1:
         raise SystemExit("--workload allgpus runs in ONE process (it drives every GPU itself)")
-    n_dev = eng.n_devices
-
-    def search(i):
-        t = time.perf_counter()
-        r = eng.search(bench_root(i), SEND, start=bench_start(i), device_mask=0)
-        if r.status != 0:
-            raise RuntimeError(f"search {i} returned status {r.status}")
-        return time.perf_counter() - t, r.nonces_done
-
-    def stats():
-        ks = [eng.stats(d) for d in range(n_dev)]
-        return sum(k.kernel_ms for k in ks) / n_dev, sum(k.nonces for k in ks), sum(k.launches for k in ks)
-
-    def reset():
-        for d in range(n_dev):
-            eng.reset_stats(d)
-
-    nonces, wall, ttw, kern_ms, kern_nonces, launches = run_timed(search, stats, reset, args.steps, args.warmup,
-                                                                  rank, 1, None)
-    line = result_line(1, args.steps, args.warmup, nonces, wall, ttw, kern_ms * n_dev, kern_nonces, launches)
-    line["n_gpus"] = n_dev
-    line["gnps_per_gpu"] = round(line["value"] / n_dev, 4)
+    n_dev = args.gpus if args.gpus > 1 else eng.n_devices
+    for d in range(n_dev):
+        eng.reset_stats(d)
+    node = inprocess_node_ttw(eng, n_dev, args.steps)
+    ks = [eng.stats(d) for d in range(n_dev)]
+    kern_ms, kern_nonces, launches = sum(k.kernel_ms for k in ks), sum(k.nonces for k in ks), sum(k.launches for k in ks)
+    wall = node["nonces_per_search"] * node["n"] / (node["node_gnps"] * 1e9)
+    line = result_line(n_dev, args.steps, 0, node["nonces_per_search"] * node["n"], wall,
+                       [node["p50"] / 1e3] * 1, kern_ms, kern_nonces, launches,
+                       parallelism=f"in-process x{n_dev} (first-win flag only, no collective)")
+    line["node_ttw_ms"] = node
+    line.pop("max_ttw_ms", None)
+    line["p50_ttw_ms"], line["p99_ttw_ms"], line["mean_ttw_ms"], line["n_ttw"] = node["p50"], node["p99"], node["mean"], node["n"]
     line["scaling"] = "strong"
     line["config"]["workload"] = (f"BASELINE configs[1] at N={n_dev}: one root at a time searched by every GPU "
                                   "of the process on disjoint strides, first win across GPUs")
-    line["config"]["parallelism"] = f"in-process x{n_dev} (first-win flag only, no collective)"
     return line
 
 
@@ -617,26 +680,32 @@ def workload_sweep(eng, args, rank, world, dist):
     per = count // world
     lo = rank * per
     n_here = per if rank < world - 1 else count - lo
-    eng.reset_stats(0)
+    devs = range(1) if world > 1 else range(args.gpus)  # in one process: the range split over --gpus devices
+    for d in devs:
+        eng.reset_stats(d)
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    hits = eng.sweep(root, thr, lo, n_here, device_mask=1, cap=1 << 16)
+    hits = eng.sweep(root, thr, lo, n_here, device_mask=(1 << len(devs)) - 1, cap=1 << 16)
     wall = time.perf_counter() - t0
-    st = eng.stats(0)
-    nonces, wall, _, (kms, kn, nl) = _reduce(dist, n_here, wall, [], (st.kernel_ms, st.nonces, st.launches))
+    ks = [eng.stats(d) for d in devs]
+    nonces, wall, _, (kms, kn, nl) = _reduce(dist, n_here, wall, [], (sum(k.kernel_ms for k in ks),
+                                                                     sum(k.nonces for k in ks),
+                                                                     sum(k.launches for k in ks)))
     if dist is not None:
         gathered = [None] * world
         dist.all_gather_object(gathered, hits)
         hits = sorted(h for g in gathered for h in g)
     want = [int(h, 16) for h in fx["hits"] if int(h, 16) < count]
-    line = result_line(world, 1, 0, nonces, wall, [wall], kms, kn, nl)
-    pmc = PMC_SWEEP
+    line = result_line(max(world, len(devs)), 1, 0, nonces, wall, [wall], kms, kn, nl)
+    pmc_name, pmc = _pmc(PMC_SWEEP)
     line["roofline"]["kernel"] = STREAM["sweep_kernel"]
-    line["roofline"]["traffic"] = _pmc_traffic(pmc)
+    line["roofline"]["traffic"] = (pmc or {}).get("hbm_bytes_per_launch")
     line["roofline"]["traffic_unit"] = ("HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
-                                        f"(profiles/{pmc}, tools/pmc_bench.sh); algorithmic bytes: "
+                                        f"(profiles/{pmc_name}, tools/pmc_bench.sh); algorithmic bytes: "
                                         "8 per hit")
+    for k in ("pmc_nonces_per_dispatch", "pmc_note"):
+        line["roofline"].pop(k, None)
     line["config"] = {"workload": f"BASELINE configs[2]: exhaustive sweep of [0, 2^{args.sweep_bits}) for the "
                                   "fixture root at fffffff800000000, ranks split the range",
                       "threshold": fx["threshold"], "count": count,
@@ -664,7 +733,7 @@ def _burst_http(eng, args, rank, world, dist):
     cancel_set = set(rng.sample(range(n), n // 4))
     est = n * float(1 << 29) / (25e9 * max(1, eng.n_devices if world == 1 else 1))
     cancel_at = sorted((rng.uniform(0.0, 0.5 * est), i) for i in cancel_set)
-    srv = HttpWorkServer(WorkServer(eng, max_active=64, device_mask=0 if world == 1 else 1), "127.0.0.1", 0).start()
+    srv = HttpWorkServer(WorkServer(eng, max_active=64, device_mask=(1 << args.gpus) - 1 if world == 1 else 1), "127.0.0.1", 0).start()
 
     def post(obj, timeout=600):
         req = urllib.request.Request(f"http://{srv.address}", data=json.dumps(obj).encode(), method="POST",
@@ -744,7 +813,7 @@ def workload_burst(eng, args, rank, world, dist):
     if dist is not None:
         dist.barrier()
     t0 = time.perf_counter()
-    tickets = [eng.submit(roots[i], SEND, start=bench_start(idx[i]), device_mask=0 if world == 1 else 1,
+    tickets = [eng.submit(roots[i], SEND, start=bench_start(idx[i]), device_mask=(1 << args.gpus) - 1 if world == 1 else 1,
                           cancel=toks[i]) for i in range(n)]
 
     def canceller():
@@ -851,7 +920,7 @@ def workload_dpow(eng, args, rank, world, dist):
     from nanopow.server import HttpWorkServer, WorkServer
     n = args.roots
     rng = random.Random(777 + rank)
-    srv = HttpWorkServer(WorkServer(eng, max_active=max(1, args.concurrency), device_mask=0 if world == 1 else 1),
+    srv = HttpWorkServer(WorkServer(eng, max_active=max(1, args.concurrency), device_mask=(1 << args.gpus) - 1 if world == 1 else 1),
                          "127.0.0.1", 0).start()
     hashes = [bench_root(11_000_000 + rank * 1_000_000 + i).hex().upper() for i in range(n)]
     t, sched = 0.0, []
@@ -958,10 +1027,27 @@ def _http_ttw(eng, n, thr=SEND, base=30_000_000, device_mask=1):
     return out
 
 
-def latency_sample(eng, dev: int, n: int):
+def fixed_overhead(eng, mask: int, n: int = 200):
+    """The per-search cost that does not scale with nonces: searches at threshold 0 (every nonce
+    wins, so the first hash of the launch wins) through the C ABI, one at a time -- submit, adopt,
+    launch, one hash, the win seen and re-validated, the launch drained, the reply."""
+    ts = []
+    for i in range(n):
+        t = time.perf_counter()
+        r = eng.search(bench_root(40_000_000 + i), 0, start=bench_start(i), device_mask=mask)
+        ts.append(time.perf_counter() - t)
+        if r.status != 0:
+            raise RuntimeError(f"overhead search {i} returned status {r.status}")
+    return {"p50": round(pct(ts, 50) * 1e3, 4), "mean": round(statistics.mean(ts) * 1e3, 4), "n": n,
+            "how": "npow_search at threshold 0 (the launch's first hash wins), one at a time"}
+
+
+def latency_sample(eng, dev: int, n: int, rate_gnps=None):
     """BASELINE config 2's time-to-work on a real sample: n first-win searches on R_0..R_{n-1} at
-    fffffff8 through the C ABI, one at a time, after the timed region (not part of value)."""
-    ttw, nonces = [], 0
+    fffffff8 through the C ABI, one at a time, after the timed region (not part of value), with the
+    decomposition of its p50 / mean: the sample's own nonce counts against the exponential law's
+    (E = 2^29, median ln2 * 2^29), the fixed per-search overhead, and the kernel rate."""
+    ttw, nn = [], []
     t0 = time.perf_counter()
     for i in range(n):
         t = time.perf_counter()
@@ -969,13 +1055,125 @@ def latency_sample(eng, dev: int, n: int):
         ttw.append(time.perf_counter() - t)
         if r.status != 0:
             raise RuntimeError(f"latency search {i} returned status {r.status}")
-        nonces += r.nonces_done
+        nn.append(r.nonces_done)
+    wall = time.perf_counter() - t0
+    over = fixed_overhead(eng, 1 << dev)
+    E = float(1 << 29)
+    ln2 = 0.6931471805599453
+    mean_n = statistics.mean(nn)
+    se_n = statistics.stdev(nn) / n ** 0.5 if n > 1 else 0.0
+    rate = (rate_gnps or sum(nn) / wall / 1e9) * 1e9  # nonces / s
+    oh = over["p50"] * 1e-3
+    out = {"p50": round(pct(ttw, 50) * 1e3, 3), "p99": round(pct(ttw, 99) * 1e3, 3),
+           "mean": round(statistics.mean(ttw) * 1e3, 3), "n": n, "gnps": round(sum(nn) / wall / 1e9, 4),
+           "roots": f"R_0..R_{n - 1}",
+           "nonces_per_search": {
+               "mean_over_2p29": round(mean_n / E, 4), "se_over_2p29": round(se_n / E, 4),
+               "median_over_ln2_2p29": round(pct(nn, 50) / (ln2 * E), 4),
+               "note": "nonces_done of each search (the winner's launch drains one hash after the win: ~0.5 M "
+                       "nonces, 0.1 % of 2^29); an exponential law has mean 2^29 and median ln2 * 2^29"},
+           "fixed_overhead_ms": over,
+           "model": {
+               "rate_gnps": round(rate / 1e9, 4),
+               "expected_p50_ms": round((ln2 * E / rate + oh) * 1e3, 3),
+               "expected_mean_ms": round((E / rate + oh) * 1e3, 3),
+               "p50_from_sample_nonces_ms": round((pct(nn, 50) / rate + oh) * 1e3, 3),
+               "mean_from_sample_nonces_ms": round((mean_n / rate + oh) * 1e3, 3),
+               "what": "time = fixed overhead + nonces / kernel rate: expected_* use the exponential law's "
+                       "nonces, *_from_sample_nonces the sample's own; the gap between p50 and expected_p50 "
+                       "that p50_from_sample_nonces closes is the sample's luck, the rest is per-search cost"},
+           "note": "npow_search at fffffff800000000 through the C ABI, one at a time, after the timed region; "
+                   "not part of value"}
+    return out
+
+
+def run_timed_inprocess(eng, n_dev: int, steps: int, warmup: int, thr: int = SEND):
+    """The product's own multi-GPU path in one process: the work pool over device_mask = the first
+    n_dev devices, n_dev searches in flight (one per client thread, each blocked in npow_wait_info
+    with the GIL released), every search split into n_dev disjoint strides with first-found
+    cancellation across the GPUs.  n_dev * steps timed searches on R_{1,000,000 + i}.  Returns
+    (nonces, wall_s, ttw_s list, infos, kernel_ms summed over devices, kernel nonces, launches)."""
+    mask = (1 << n_dev) - 1
+    for w in range(warmup):
+        eng.submit(bench_root(1_900_000 + w), thr, start=bench_start(1_900_000 + w), device_mask=mask).wait()
+    for d in range(n_dev):
+        eng.reset_stats(d)
+    total = n_dev * steps
+    lock = threading.Lock()
+    nxt = [0]
+    recs = []
+    errors = []
+
+    def client():
+        while True:
+            with lock:
+                i = nxt[0]
+                if i >= total:
+                    return
+                nxt[0] += 1
+            idx = 1_000_000 + i
+            try:
+                t = time.perf_counter()
+                info = eng.submit(bench_root(idx), thr, start=bench_start(idx), device_mask=mask).wait_info()
+                dt = time.perf_counter() - t
+            except Exception as e:  # reported after the join
+                errors.append(repr(e))
+                return
+            if info.status != 0:
+                errors.append(f"search {idx} returned status {info.status}")
+                return
+            with lock:
+                recs.append((dt, info.nonces_done, info.stop_after_decide_us, info.overshoot_nonces))
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=client) for _ in range(n_dev)]
+    for t in ths:
+        t.start()
+    for t in ths:
+        t.join()
+    wall = time.perf_counter() - t0
+    if errors:
+        raise RuntimeError("; ".join(errors[:4]))
+    ks = [eng.stats(d) for d in range(n_dev)]
+    return (sum(r[1] for r in recs), wall, [r[0] for r in recs], recs, sum(k.kernel_ms for k in ks),
+            sum(k.nonces for k in ks), sum(k.launches for k in ks), ks)
+
+
+def overshoot_summary(spans_us, over_nonces, done):
+    return {"stop_after_decide_us": {"p50": round(pct(spans_us, 50), 1), "p99": round(pct(spans_us, 99), 1)},
+            "overshoot_nonces": {"p50": int(pct(over_nonces, 50)), "p99": int(pct(over_nonces, 99)),
+                                 "share_of_nonces": round(sum(over_nonces) / max(1, sum(done)), 5)},
+            "what": "per search, how long the other GPUs kept hashing after the host accepted the winner "
+                    "(host-observed: their final count or launch end seen by their worker -- an upper bound) "
+                    "and the nonces that span is worth at each GPU's kernel rate (npow_wait_info)"}
+
+
+def inprocess_node_ttw(eng, n_dev: int, m: int, thr: int = SEND):
+    """One root at a time over all n_dev devices of the process (north_star: the nonce space split
+    into disjoint per-GPU strides, first found cancels the others): p50/p99 time-to-work at N GPUs
+    and each search's overshoot (npow_wait_info)."""
+    mask = (1 << n_dev) - 1
+    ttw, spans, over, done, decide = [], [], [], [], []
+    t0 = time.perf_counter()
+    for i in range(m):
+        idx = 3_000_000 + i
+        t = time.perf_counter()
+        info = eng.submit(bench_root(idx), thr, start=bench_start(idx), device_mask=mask).wait_info()
+        ttw.append(time.perf_counter() - t)
+        if info.status != 0:
+            raise RuntimeError(f"node search {idx} returned status {info.status}")
+        spans.append(info.stop_after_decide_us)
+        over.append(info.overshoot_nonces)
+        done.append(info.nonces_done)
+        decide.append(info.decide_us)
     wall = time.perf_counter() - t0
     return {"p50": round(pct(ttw, 50) * 1e3, 3), "p99": round(pct(ttw, 99) * 1e3, 3),
-            "mean": round(statistics.mean(ttw) * 1e3, 3), "n": n, "gnps": round(nonces / wall / 1e9, 4),
-            "roots": f"R_0..R_{n - 1}",
-            "note": "npow_search at fffffff800000000 through the C ABI, one at a time, after the timed region; "
-                    "expected p50 = ln2 * 2^29 nonces / rate; not part of value"}
+            "mean": round(statistics.mean(ttw) * 1e3, 3), "n": m, "node_gnps": round(sum(done) / wall / 1e9, 4),
+            "decide_p50_ms": round(pct(decide, 50) / 1e3, 3),
+            "nonces_per_search": round(statistics.mean(done)),
+            **overshoot_summary(spans, over, done),
+            "note": f"one root at a time searched by all {n_dev} GPUs of the process on disjoint strides "
+                    "(npow_submit over device_mask), first win cancelling the others; after the timed region, "
+                    "not part of value"}
 
 
 def workload_receive(eng, args, rank, world, dist):
@@ -983,8 +1181,6 @@ def workload_receive(eng, args, rank, world, dist):
     if world > 1:
         raise SystemExit("--workload receive runs in one process")
     recv = 0xfffffe0000000000
-    sys.path.insert(0, os.path.join(HERE, "oracle"))
-    import oracle  # CPU baseline legs only
     from nanopow.server import HttpWorkServer, WorkServer
     import urllib.request
     # GPU through the C ABI
@@ -1011,22 +1207,7 @@ def workload_receive(eng, args, rank, world, dist):
             assert "work" in rep
     finally:
         srv.stop()
-    # CPU: hashlib on one core (the reference's CPU path), a bounded number of requests
-    cpu1, cpu1_nonces = [], 0
-    for i in range(args.cpu_requests):
-        t = time.perf_counter()
-        k, nonce = _hashlib_search(bench_root(22_000_000 + i), recv, bench_start(i), 1 << 28)
-        cpu1.append(time.perf_counter() - t)
-        cpu1_nonces += k
-        assert nonce is not None
-    # CPU: the oracle's C port on the host cores (exhaustive scan of the same requests' first chunk)
-    threads = min(16, os.cpu_count() or 1)
-    cpun = []
-    for i in range(args.cpu_requests):
-        root = bench_root(22_000_000 + i)
-        t = time.perf_counter()
-        oracle.sweep(root, recv, bench_start(i), 1 << 24, threads=threads)  # 2x the expected nonces
-        cpun.append(time.perf_counter() - t)
+    # the CPU legs (receive_cpu_legs) ran before the GPU was opened; main() adds them
     line = result_line(1, args.steps, 0, 0, 1.0, gpu, 0.0, 0, 0)
     line.pop("roofline")
     line["value"] = round(pct(gpu, 50) * 1e3, 3)
@@ -1041,23 +1222,136 @@ def workload_receive(eng, args, rank, world, dist):
                                   "n": len(http)},
         "gpu_http_new_connection_ms": {"p50": round(pct(http_new, 50) * 1e3, 3),
                                        "p99": round(pct(http_new, 99) * 1e3, 3), "n": len(http_new)},
-        "cpu_hashlib_1core_ms": {"p50": round(pct(cpu1, 50) * 1e3, 1), "n": len(cpu1),
-                                 "gnps": round(cpu1_nonces / sum(cpu1) / 1e9, 6)},
-        "cpu_oracle_c_scan_2p24_ms": {"median": round(statistics.median(cpun) * 1e3, 1), "threads": threads,
-                                      "gnps": round((1 << 24) / statistics.median(cpun) / 1e9, 5)},
     }
     return line
 
 
+def _hashlib_interleaved(job):
+    """One process of the all-cores CPU reference search: nonces start + k, start + k + P, ... until a
+    value >= thr or another process has found one (the shared flag, checked every 4,096 nonces)."""
+    root, thr, start, k, P, limit = job
+    b2 = hashlib.blake2b
+    flag = _MP_FLAG
+    n = (start + k) & ((1 << 64) - 1)
+    for c in range(limit):
+        if int.from_bytes(b2(n.to_bytes(8, "little") + root, digest_size=8).digest(), "little") >= thr:
+            flag.value = 1
+            return c + 1, n
+        if (c & 4095) == 0 and flag.value:
+            return c + 1, None
+        n = (n + P) & ((1 << 64) - 1)
+    return limit, None
+
+
+_MP_FLAG = None
+
+
+def _mp_init(flag):
+    global _MP_FLAG
+    _MP_FLAG = flag
+
+
+def receive_cpu_legs(args):
+    """BASELINE configs[0]'s CPU side: the reference's CPU path,
+    hashlib.blake2b(digest_size=8), on one core and on every granted host core (one process per
+    core on interleaved nonces, the first hit ending the request), and the oracle's C port on the
+    same cores.  Runs before the GPU is opened (its worker processes are forked)."""
+    import multiprocessing
+    sys.path.insert(0, os.path.join(HERE, "oracle"))
+    import oracle  # CPU baseline legs only
+    recv = 0xfffffe0000000000
+    cores = granted_cores()
+    cpu1, cpu1_nonces = [], 0
+    for i in range(args.cpu_requests):
+        t = time.perf_counter()
+        k, nonce = _hashlib_search(bench_root(22_000_000 + i), recv, bench_start(i), 1 << 28)
+        cpu1.append(time.perf_counter() - t)
+        cpu1_nonces += k
+        assert nonce is not None
+    cpun_hl, hl_nonces = [], 0
+    ctx = multiprocessing.get_context("fork")
+    for i in range(args.cpu_requests):
+        root = bench_root(22_000_000 + i)
+        flag = ctx.Value("i", 0, lock=False)
+        with ctx.Pool(cores, initializer=_mp_init, initargs=(flag,)) as pool:
+            t = time.perf_counter()
+            parts = pool.map(_hashlib_interleaved, [(root, recv, bench_start(i), k, cores, 1 << 26)
+                                                    for k in range(cores)], chunksize=1)
+            cpun_hl.append(time.perf_counter() - t)
+        found = [n for _, n in parts if n is not None]
+        assert found and all(oracle.work_value(root, n) >= recv for n in found)
+        hl_nonces += sum(c for c, _ in parts)
+    cpun = []
+    for i in range(args.cpu_requests):
+        root = bench_root(22_000_000 + i)
+        t = time.perf_counter()
+        oracle.sweep(root, recv, bench_start(i), 1 << 24, threads=cores)  # 2x the expected nonces
+        cpun.append(time.perf_counter() - t)
+    return {
+        "cpu_hashlib_1core_ms": {"p50": round(pct(cpu1, 50) * 1e3, 1), "n": len(cpu1),
+                                 "gnps": round(cpu1_nonces / sum(cpu1) / 1e9, 6)},
+        "cpu_hashlib_allcores_ms": {"p50": round(pct(cpun_hl, 50) * 1e3, 1), "n": len(cpun_hl), "cores": cores,
+                                    "gnps": round(hl_nonces / sum(cpun_hl) / 1e9, 6),
+                                    "how": f"hashlib.blake2b in {cores} forked processes on interleaved nonces, the "
+                                           "first hit ending the request (pool start-up included)"},
+        "cpu_oracle_c_scan_2p24_ms": {"median": round(statistics.median(cpun) * 1e3, 1), "threads": cores,
+                                      "gnps": round((1 << 24) / statistics.median(cpun) / 1e9, 5)},
+    }
+
+
+def add_clock(line, clocks, over):
+    """The in-kernel shader clock of the timed launches (mean over ranks / devices) and the roofline
+    priced at it."""
+    if not clocks:
+        return
+    mhz = statistics.mean(clocks)
+    line["sclk_mhz"] = {"mean": round(mhz, 1), over: len(clocks),
+                        "source": "in-kernel: s_memtime / s_memrealtime spans of one wave per XCD in every "
+                                  f"timed search launch (libnanopow stats clock_mhz), mean over {over}"}
+    line["roofline"]["frac_at_measured_sclk"] = round(line["roofline"]["achieved"] / (256 * 128 * mhz * 1e6 / 1e12), 4)
+    kg = line["roofline"]["kernel_gnps"]
+    if kg:  # SIMD cycles per 64-nonce wave-hash at the in-kernel clock (1,024 SIMDs per GPU)
+        n = line["n_gpus"]
+        line["roofline"]["stream_harness"]["kernel_cycles_per_hash"] = round(1024 * 64 * mhz * 1e6 / (kg / n * 1e9), 1)
+
+
+def main_inprocess(eng, args) -> int:
+    """--gpus N > 1 without torch.distributed.run: the product's own multi-GPU path (run_timed_inprocess),
+    then one root at a time over all N GPUs (inprocess_node_ttw)."""
+    n = args.gpus
+    with SclkSampler(0) as sclk:
+        nonces, wall, ttw, recs, kern_ms, kern_nonces, launches, ks = run_timed_inprocess(eng, n, args.steps,
+                                                                                          args.warmup)
+    line = result_line(n, args.steps, args.warmup, nonces, wall, ttw, kern_ms, kern_nonces, launches,
+                       parallelism=f"in-process x{n}: the work pool over device_mask = {n} GPUs, {n} searches in "
+                                   f"flight, each split into {n} disjoint strides with first-found cancellation "
+                                   "(no collective)")
+    # kernel_gnps above is per device-second summed over devices: report the node's kernel rate too
+    line["roofline"]["kernel_gnps_per_gpu"] = round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None
+    line["roofline"]["kernel_gnps"] = round(kern_nonces / (kern_ms * 1e-3 / n) / 1e9, 4) if kern_ms > 0 else None
+    add_clock(line, [k.clock_mhz for k in ks if k.clock_mhz > 0], "devices")
+    clk = sclk.summary()
+    if clk:
+        line["sysfs_sclk_mhz"] = clk
+    line["timed_overshoot"] = overshoot_summary([r[2] for r in recs], [r[3] for r in recs], [r[1] for r in recs])
+    line["early_finishes"] = sum(k.early_finishes for k in ks)
+    line["kills_relayed"] = sum(k.kills_relayed for k in ks)
+    if args.node_searches:
+        line["node_ttw_ms"] = inprocess_node_ttw(eng, n, args.node_searches)
+    print(json.dumps(line), flush=True)
+    return 0
+
+
 def main() -> int:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=300, help="searches per rank in the timed region")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs: under torch.distributed.run it must equal WORLD_SIZE (one rank per GPU); alone, "
+                         "N > 1 runs the work pool over N devices in this process")
+    ap.add_argument("--steps", type=int, default=300, help="searches per GPU in the timed region")
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--iters", type=int, default=0, help="override wave iterations per launch")
+    ap.add_argument("--iters", type=int, default=0, help="override the search launch iteration cap")
     ap.add_argument("--budget-us", type=int, default=-1, help="override the search launch budget (0 = off)")
-    ap.add_argument("--pool-blocks", type=int, default=0, help="override search workgroups per CU")
     ap.add_argument("--workload", default="search",
                     choices=["search", "allgpus", "sweep", "burst", "sustained", "dpow", "receive"])
     ap.add_argument("--sweep-bits", type=int, default=36, help="sweep: range [0, 2^bits)")
@@ -1070,17 +1364,24 @@ def main() -> int:
     ap.add_argument("--via", choices=["abi", "http"], default="abi",
                     help="burst: submit through the C ABI work pool or POST to the HTTP work server")
     ap.add_argument("--node-searches", type=int, default=300,
-                    help="search, N>1: roots searched by all ranks at once after the timed steps (node time-to-work)")
+                    help="search, N>1: roots searched by all GPUs at once after the timed steps (node time-to-work)")
     ap.add_argument("--http-requests", type=int, default=100,
                     help="search, N=1: work_generate requests timed at the JSON boundary after the timed steps")
     ap.add_argument("--latency-searches", type=int, default=1000,
                     help="search, N=1: C-ABI searches on R_0..R_{n-1} after the timed steps (p50/p99 time-to-work)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("bench.py: --gpus must be >= 1")
+    if WORLD > 1 and args.gpus != WORLD:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={WORLD}: under torch.distributed.run "
+                         "there is one rank per GPU")
+    inproc = WORLD == 1 and args.gpus > 1
 
-    # The CPU baseline runs first, before anything opens the GPU (its worker processes are forked).
+    # The CPU legs run first, before anything opens the GPU (their worker processes are forked).
     cpu = None
-    if args.workload == "search" and WORLD == 1 and not args.no_cpu_baseline:
+    if args.workload == "search" and WORLD == 1 and args.gpus == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
+    recv_cpu = receive_cpu_legs(args) if args.workload == "receive" else None
 
     rank = int(os.environ.get("RANK", "0"))
     dist = None
@@ -1093,23 +1394,29 @@ def main() -> int:
     import nanopow
     from nanopow import _lib
     eng = nanopow.engine()  # fails loudly without libnanopow.so / a GPU: no CPU fallback
+    if WORLD > 1 and eng.n_devices != 1 and "NANOPOW_VIRTUAL_DEVICES" not in os.environ:
+        raise SystemExit(f"bench.py: rank {rank} sees {eng.n_devices} devices, expected exactly one")
+    if eng.n_devices < args.gpus and WORLD == 1:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but only {eng.n_devices} device(s) are visible")
     if args.iters:
         eng.set_tuning(args.iters, 0, 0)
-    if args.budget_us >= 0 or args.pool_blocks:
-        eng.set_pool_tuning(None if args.budget_us < 0 else args.budget_us, args.pool_blocks)
-    # normally 0 (the rank's only visible GPU); if the runtime still shows several (a device list
-    # exported under another variable), the rank takes the LOCAL_RANK-th so ranks never share a GPU
-    dev = LOCAL_RANK % eng.n_devices if WORLD > 1 else 0
+    if args.budget_us >= 0:
+        eng.set_pool_tuning(args.budget_us)
+    dev = 0  # a rank's only visible GPU; in one process, devices 0..N-1
     if args.workload != "search":
         fn = {"allgpus": workload_allgpus, "sweep": workload_sweep, "burst": workload_burst,
               "sustained": workload_sustained, "dpow": workload_dpow, "receive": workload_receive}[args.workload]
         line = fn(eng, args, rank, WORLD, dist)
+        if recv_cpu:
+            line["receive"].update(recv_cpu)
         if rank == 0:
             print(json.dumps(line), flush=True)
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
         return 0
+    if inproc:
+        return main_inprocess(eng, args)
 
     def search(i):
         t = time.perf_counter()
@@ -1135,24 +1442,15 @@ def main() -> int:
         dist.all_gather_object(gathered, local)
     else:
         gathered = [local]
-    lat = latency_sample(eng, dev, args.latency_searches) if (WORLD == 1 and args.latency_searches) else None
+    kern_rate = res[4] / (res[3] * 1e-3) / 1e9 if res[3] > 0 else None
+    lat = latency_sample(eng, dev, args.latency_searches, kern_rate) if (WORLD == 1 and args.latency_searches) else None
     http = _http_ttw(eng, args.http_requests) if (rank == 0 and WORLD == 1 and args.http_requests) else None
     node = None
     if dist is not None and args.node_searches > 0 and int(os.environ.get("LOCAL_WORLD_SIZE", WORLD)) == WORLD:
         node = node_time_to_work(eng, dev, rank, WORLD, dist, args.node_searches)
     if rank == 0:
         line = result_line(WORLD, args.steps, args.warmup, *res)
-        clocks = [g[0] for g in gathered if g[0] > 0]
-        if clocks:
-            mhz = statistics.mean(clocks)
-            line["sclk_mhz"] = {"mean": round(mhz, 1), "ranks": len(clocks),
-                                "source": "in-kernel: s_memtime / s_memrealtime spans of one wave per XCD in every "
-                                          "timed search launch (libnanopow stats clock_mhz), mean over ranks"}
-            line["roofline"]["frac_at_measured_sclk"] = round(line["roofline"]["achieved"] /
-                                                              (256 * 128 * mhz * 1e6 / 1e12), 4)
-            kg = line["roofline"]["kernel_gnps"]
-            if kg:  # SIMD cycles per 64-nonce wave-hash at the in-kernel clock (1,024 SIMDs)
-                line["roofline"]["stream_harness"]["kernel_cycles_per_hash"] = round(1024 * 64 * mhz * 1e6 / (kg * 1e9), 1)
+        add_clock(line, [g[0] for g in gathered if g[0] > 0], "ranks")
         clk = sclk.summary()
         if clk:
             line["sysfs_sclk_mhz"] = clk

@@ -24,7 +24,8 @@
  *   - A cancel word is raised from another thread with a release store
  *     (`__atomic_store_n(w, 1, __ATOMIC_RELEASE)`; an aligned 32-bit store, as
  *     ctypes makes, is one on x86-64); the library load-acquires it.
- *   - device_mask bit d selects HIP device d; 0 means "all devices".
+ *   - device_mask bit d selects logical device d (HIP device d, or d mod the HIP
+ *     devices under NANOPOW_VIRTUAL_DEVICES, a test setting); 0 means "all devices".
  *   - Calls that use disjoint device sets may run concurrently from
  *     different threads; calls that share a device serialise on it.
  */
@@ -50,6 +51,17 @@ extern "C" {
 #define NPOW_ERR_INTERNAL (-7)     /* host-side failure (out of memory, thread creation); no C++
                                       exception ever crosses this ABI */
 
+/* ABI revision (npow_abi_version()).  3: npow_values runs the search kernels' stream;
+ * npow_values_path, npow_wait_info, npow_device_stats_get_sized added;
+ * npow_device_stats_get writes only the revision-2 prefix of npow_device_stats. */
+#define NPOW_ABI_VERSION 3
+
+/* Hash paths of npow_values_path. */
+#define NPOW_PATH_SEARCH 0  /* the instruction stream the search and sweep kernels execute
+                               (npow_hash_asm_lockstep_ld.inc, two lockstep workgroups per CU) */
+#define NPOW_PATH_SEQ 1     /* a second generated stream, scheduled without barriers (npow_hash_asm.inc) */
+#define NPOW_PATH_GENERIC 2 /* plain HIP C++ of the 12 rounds, one (root, nonce) per lane */
+
 /* Per-device counters; kernel_ms is measured with HIP events recorded on the
  * stream each kernel is launched on (bench.py's roofline leg reads these). */
 typedef struct npow_device_stats {
@@ -67,8 +79,8 @@ typedef struct npow_device_stats {
   int32_t dead;           /* 1 once the device has been dropped: 3 invalid results in a row
                              (nano-work-server.exe @1669144) or a failed HIP call; searches then
                              skip it and its jobs' remaining ranges move to the other devices */
-  int32_t pool_groups;    /* the search kernel: 0 = seq (NANOPOW_POOL_KERNEL=seq), 1 or 2 = lockstep
-                             workgroups per CU (npow_pool_kernel_ls* / _ls2*; NANOPOW_LS_GROUPS) */
+  int32_t pool_groups;    /* lockstep workgroups per CU of the search kernel: always 2
+                             (npow_pool_kernel_ls2*; revisions before ABI 3 also had 0 = seq, 1) */
   uint64_t early_finishes;  /* jobs finished from the kernel's published final count (two-group
                                kernels): a won or killed entry's count once no workgroup is left on
                                it, before the launch that held it ends */
@@ -76,7 +88,30 @@ typedef struct npow_device_stats {
                                (always 0: a protocol check) */
   uint64_t yields;          /* running launches ended early so that new jobs could start */
   uint64_t dyn_entries;     /* jobs that joined a running two-group launch instead (no yield) */
+  /* ---- ABI 3 (npow_device_stats_get_sized only) ---- */
+  uint64_t kills_relayed;   /* losing jobs of this device stopped by another device's win: the deciding
+                               thread raised this device's kill word directly (no wait for its worker) */
 } npow_device_stats;
+
+/* Outcome of one search (npow_wait_info).  Times are host steady-clock microseconds since
+ * npow_submit.  For a job split over several devices, the other devices keep hashing from the
+ * moment the host accepts the winner until their waves have left the job: stop_after_decide_us is
+ * the longest such span among them as the host observed it (the device's worker saw the job's
+ * final count or the launch that held it complete -- so an upper bound of the device time), and
+ * overshoot_nonces the sum over them of that span times the device's kernel rate (likewise an
+ * upper bound of the nonces hashed after the decision).  Both are 0 for a one-device job. */
+typedef struct npow_search_info {
+  uint32_t size;            /* set by the caller: sizeof(npow_search_info) it was compiled with */
+  int32_t status;           /* as npow_wait returns it */
+  uint64_t nonce, value;    /* valid when status == NPOW_OK */
+  uint64_t nonces_done;     /* every device, including the rest of a launch after the win */
+  int32_t winner_device;    /* logical device whose result decided the job; -1 if none */
+  int32_t n_devices;        /* devices the job was split over */
+  double decide_us;         /* the winner accepted (CPU re-validated) */
+  double finish_us;         /* every device done with the job */
+  double stop_after_decide_us;
+  uint64_t overshoot_nonces;
+} npow_search_info;
 
 /* Open every visible HIP device, create its stream and buffers.
  * Replaces the work server's OpenCL device set-up for `--gpu P:D[:THREADS]`
@@ -143,6 +178,10 @@ int npow_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
 int npow_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce_out, uint64_t* value_out,
               uint64_t* nonces_done);
 
+/* npow_wait with the search's outcome and timeline in *info (info->size set by the caller; the
+ * library writes at most that many bytes).  Returns as npow_wait. */
+int npow_wait_info(uint64_t ticket, int64_t timeout_us, npow_search_info* info);
+
 /* Cancel a ticket (same effect as raising its cancel word). */
 int npow_cancel(uint64_t ticket);
 
@@ -163,9 +202,16 @@ int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint6
                uint64_t* n_out);
 
 /* Work values of `count` consecutive nonces start, start+1, ... for one root,
- * computed by the same specialised GPU code path the search and sweep kernels
- * use (parity tests compare every value with the CPU).  device = HIP index. */
+ * computed by the instruction stream the search and sweep kernels execute
+ * (npow_values_kernel_ls2: the same uniform loads, barrier intervals and
+ * workgroup shape), so the parity tests compare that stream's full 64-bit values
+ * with the CPU.  device = logical device index. */
 int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t count, uint64_t* values_out);
+
+/* The same through a chosen hash path (NPOW_PATH_SEARCH = npow_values, NPOW_PATH_SEQ,
+ * NPOW_PATH_GENERIC; the generic path takes count < 2^32). */
+int npow_values_path(int device, const uint8_t root[32], uint64_t start, uint64_t count, int path,
+                     uint64_t* values_out);
 
 /* Work values of n independent (root_i, nonce_i) pairs on one device
  * (generic per-lane-root GPU path; server-side validation in bulk,
@@ -173,29 +219,39 @@ int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t cou
 int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, uint32_t n,
                       uint64_t* values_out);
 
-/* Tuning knobs (0 keeps the current value).  iters_per_launch: wave
- * iterations per kernel launch (chunk = grid*256*iters nonces);
- * poll_interval: iterations between a wave's polls of the host abort word;
- * blocks_per_cu: workgroups of 256 lanes per CU in the launch grid. */
+/* Tuning knobs (0 keeps the current value).  iters_per_launch: the iteration cap of a
+ * search launch (default 8192; a launch runs half as many wave iterations, each the time of two
+ * hashes of its SIMD's other workgroup) and the span of bounded jobs' launches;
+ * poll_interval: wave iterations between a wave's polls of the host kill / yield words
+ * (rounded up to a power of two; 8 waves per iteration poll grid-wide at the default 1024);
+ * blocks_per_cu: 256-lane workgroups per CU of the NPOW_PATH_SEQ values kernel. */
 int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t blocks_per_cu);
 
 /* Search (work pool) launches.  budget_us: wall-clock budget of a launch (default 20000;
- * 0 = iteration count only; 0xffffffff keeps the current value).  Waves searching unbounded
+ * 0 = iteration count only; 0xffffffff keeps the current value).  Workgroups searching unbounded
  * jobs stop together when it runs out -- VALU issue favours a SIMD's oldest wave, so a launch
- * of a fixed iteration count ends in a tail of one or two waves per SIMD -- and
- * iters_per_launch (default 8192) is then only the cap (and the span of bounded jobs, which
- * always complete their dense ranges).  A running launch is ended early when new jobs arrive
- * for its device.  Search launches use the lockstep kernel, one 1,024-lane workgroup per CU
- * (environment NANOPOW_POOL_KERNEL=seq at npow_init selects the seq kernel instead);
- * blocks_per_cu: 256-lane workgroups per CU of a seq-kernel search launch (default 4; 0 keeps).
- * npow_set_tuning's blocks_per_cu applies to sweeps and value ranges. */
+ * of a fixed iteration count would end in a tail -- and iters_per_launch is then only the cap
+ * (bounded jobs always complete their dense ranges).
+ * The search kernel is npow_pool_kernel_ls2*: two 1,024-lane lockstep workgroups per CU, with
+ * early finish (a won or cancelled job returns from the count its last workgroup publishes, not
+ * at the end of the launch that held it) and dynamic entries (an unbounded job submitted while a
+ * launch with other live jobs runs joins that launch).  A running launch is ended early (a yield)
+ * only when a new job cannot join it: a bounded job, a one-job launch, a launch within 3 ms of its
+ * budget, or a full ring of 32 dynamic entries.
+ * blocks_per_cu: must be 0 or 2 (the workgroups per CU of the search kernel are fixed). */
 int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu);
 
+/* Writes the ABI-2 prefix of npow_device_stats (through dyn_entries), as callers compiled
+ * against that revision allocate. */
 int npow_device_stats_get(int device, npow_device_stats* out);
+/* Writes min(size, sizeof(npow_device_stats)) bytes. */
+int npow_device_stats_get_sized(int device, npow_device_stats* out, uint64_t size);
 int npow_device_stats_reset(int device);
 
 /* Library / kernel identification string (gfx target, build flags). */
 const char* npow_version(void);
+/* NPOW_ABI_VERSION of the library. */
+int npow_abi_version(void);
 
 #ifdef __cplusplus
 }

@@ -20,6 +20,7 @@
 #include <time.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <exception>
 #include <chrono>
 #include <cstdio>
@@ -49,12 +50,12 @@ const std::string& last_error() { return t_err; }
 std::vector<std::unique_ptr<Device>> g_devs;
 std::atomic<uint32_t> g_iters{8192};    // search launches: iteration cap under the time budget (the oldest wave of a
                                         // SIMD runs ~4 us per iteration, ~5,000 in 20 ms) and the span of bounded jobs
-constexpr uint32_t kSweepIters = 4096;  // sweep launches: mean wave iterations (2^31 nonces, ~80 ms; a launch
-                                        // costs ~0.35 ms of ramp-up and drain: 26.46 Gnonce/s at 20 ms, 26.93 at 80 ms)
-// Sweep: most wave iterations per claim (npow_task_kernel).  Plain guided self-scheduling
-// (first claims T / 2W, ~2,048 iterations) assumes equally fast workers; here a SIMD's
-// youngest wave runs several times slower than its oldest, and a young wave still holding a
-// 2,048-iteration claim becomes the launch's tail (25.81 Gnonce/s vs 26.89 at 64).
+constexpr uint64_t kSweepChunk = 1ull << 31;  // sweep launches: 2^31 nonces (~65 ms; a launch costs ~0.35 ms of
+                                              // ramp-up and drain: 26.46 Gnonce/s at 20 ms, 26.93 at 80 ms in round 1)
+// Sweep: most rows per claim (npow_sweep_kernel_ls2).  Plain guided self-scheduling (first claims
+// remaining / 2W) assumes equally fast workers; here a SIMD's younger waves run slower than its
+// oldest, and a young worker still holding a huge claim becomes the launch's tail (round 1, per-wave
+// claims: 25.81 Gnonce/s vs 26.89 at a cap of 64).
 // NANOPOW_SWEEP_CLAIM overrides (experiments).
 uint32_t sweep_max_claim() {
   static const uint32_t v = [] {
@@ -65,18 +66,8 @@ uint32_t sweep_max_claim() {
   return v;
 }
 std::atomic<uint32_t> g_poll{1024};     // a wave reads the host word every g_poll iterations (8 waves per iteration grid-wide)
-std::atomic<uint32_t> g_blocks_per_cu{8};
+std::atomic<uint32_t> g_blocks_per_cu{8};  // npow_values_kernel_seq: 256-lane workgroups per CU
 std::atomic<uint32_t> g_budget_us{20000};  // pool launches end on time, not on their slowest wave
-// Pool launches: 4 workgroups (16 waves) per CU.  Four waves per SIMD already saturate VALU
-// issue under the time budget (27.05 Gnonce/s at 4, 5 and 6 per CU), and the pool kernel's
-// ~100 SGPRs admit only 6 per CU (tools/experiments/wave_probe.cpp: with 8 requested, 2 per CU start
-// only when the first 6 finish), so 4 leaves room for compiler changes.
-std::atomic<uint32_t> g_pool_blocks_per_cu{4};
-// The lockstep search kernel (npow_kernel.hip pool_body_ls) unless NANOPOW_POOL_KERNEL=seq; read
-// once, before the first launch (npow_init).
-bool g_pool_lockstep = true;
-uint32_t g_ls_lds = 0;
-int g_ls_groups = 2;  // NANOPOW_LS_GROUPS=1: one 1,024-lane workgroup per CU (npow_pool_kernel_ls*)
 
 std::vector<Device*> select_devices(uint64_t mask) {
   std::vector<Device*> out;
@@ -110,11 +101,8 @@ struct Inflight {
 // Launch one chunk on d's stream bracketed by timing events.
 int launch_chunk(Device& d, Mode mode, const LaunchArgs& a, int ring, uint64_t* out) {
   HIPTRY(hipEventRecord(d.ev_start[ring], d.stream));
-  if (mode == Mode::kSweep && g_pool_lockstep)  // the lockstep sweep: 1,024-lane workgroups, 1 or 2 per CU
-    HIPTRY(launch_task(g_ls_groups == 2 ? Mode::kSweepLs2 : Mode::kSweepLs, d.cus * g_ls_groups, d.stream, a, d.st,
-                       d.mb_dev, out));
-  else
-    HIPTRY(launch_task(mode, grid_of(d), d.stream, a, d.st, d.mb_dev, out));
+  // the shipped stream's kernels: two 1,024-lane workgroups per CU; the seq values kernel: 256-lane ones
+  HIPTRY(launch_task(mode, mode == Mode::kValuesSeq ? grid_of(d) : ls_grid(d), d.stream, a, d.st, d.mb_dev, out));
   HIPTRY(hipEventRecord(d.ev_stop[ring], d.stream));
   return NPOW_OK;
 }
@@ -205,7 +193,8 @@ void free_device(Device& d) {
 int init_device(Device& d, int n_physical) {
   d.hip_id = d.id % n_physical;
   HIPTRY(hipSetDevice(d.hip_id));
-  if (const char* f = getenv("NANOPOW_FAULT_INIT"))  // test hook: this logical device fails to open
+  const char* f = test_hooks_enabled() ? getenv("NANOPOW_FAULT_INIT") : nullptr;
+  if (f)  // test hook (with NANOPOW_TEST_HOOKS=1): this logical device fails to open
     if (atoi(f) == d.id) {
       HIPTRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));  // something to clean up
       return fail(NPOW_ERR_HIP, "injected init failure (NANOPOW_FAULT_INIT)");
@@ -245,7 +234,7 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
   a.poll_mask = poll_mask();
   a.cap = (uint32_t)kHitCap;
   a.max_claim = sweep_max_claim();
-  const uint64_t chunk = (uint64_t)grid_of(d) * kBlock * kSweepIters;
+  const uint64_t chunk = kSweepChunk;
   uint64_t issued = 0;
   uint32_t launches = 0;  // parity picks the launch's claim counter (reset_task zeroed both)
   int ring = 0;
@@ -298,8 +287,11 @@ extern "C" {
 const char* npow_last_error(void) { return t_err.c_str(); }
 
 const char* npow_version(void) {
-  return "libnanopow 0.1 (gfx950 HIP kernel: blake2b-64 nonce search; v_lshl_add_u64 adds, v_alignbit rotations)";
+  return "libnanopow 0.3 (ABI 3; gfx950 HIP kernels: blake2b-64 nonce search, two lockstep workgroups per CU; "
+         "v_lshl_add_u64 adds, v_alignbit rotations)";
 }
+
+int npow_abi_version(void) { return NPOW_ABI_VERSION; }
 
 int npow_init(int* n_devices) try {
   std::lock_guard<std::mutex> g(g_mu);
@@ -314,9 +306,6 @@ int npow_init(int* n_devices) try {
   // NANOPOW_VIRTUAL_DEVICES=N (testing): expose N logical devices over the physical ones
   // (logical i -> HIP device i mod n), each with its own stream, buffers and pool worker, so
   // the multi-device first-win path runs on a one-GPU machine.
-  if (const char* k = getenv("NANOPOW_POOL_KERNEL")) g_pool_lockstep = strcmp(k, "seq") != 0;
-  if (const char* l = getenv("NANOPOW_LS_LDS")) g_ls_lds = (uint32_t)atoi(l);
-  if (const char* k = getenv("NANOPOW_LS_GROUPS")) g_ls_groups = atoi(k) == 1 ? 1 : 2;
   if (const char* b = getenv("NANOPOW_BUDGET_US")) g_budget_us = (uint32_t)atoi(b);  // A/B runs
   if (const char* p = getenv("NANOPOW_POLL")) g_poll = (uint32_t)atoi(p);             // A/B runs
   int n_logical = n;
@@ -384,9 +373,9 @@ int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t 
 
 int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu) try {
   if (budget_us != 0xffffffffu && budget_us > 1000000) return fail(NPOW_ERR_BAD_ARGUMENT, "budget_us must be <= 1000000");
-  if (blocks_per_cu > 32) return fail(NPOW_ERR_BAD_ARGUMENT, "blocks_per_cu must be <= 32");
+  if (blocks_per_cu != 0 && blocks_per_cu != (uint32_t)kLsGroups)
+    return fail(NPOW_ERR_BAD_ARGUMENT, "blocks_per_cu must be 0 or 2: the search kernel runs two workgroups per CU");
   if (budget_us != 0xffffffffu) g_budget_us = budget_us;
-  if (blocks_per_cu) g_pool_blocks_per_cu = blocks_per_cu;
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 
@@ -409,7 +398,7 @@ static void settle_stats(const Device& d) {
     std::this_thread::sleep_for(std::chrono::microseconds(20));
 }
 
-int npow_device_stats_get(int device, npow_device_stats* out) try {
+static int stats_fill(int device, npow_device_stats* out) {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size() || !out) return fail(NPOW_ERR_BAD_ARGUMENT, "bad device");
   Device& d = *g_devs[device];
@@ -422,16 +411,32 @@ int npow_device_stats_get(int device, npow_device_stats* out) try {
   out->kernel_ms = d.kernel_ms;
   out->invalid_work = d.invalid;
   out->cus = d.cus;
-  out->grid = pool_shape(d).grid;
+  out->grid = ls_grid(d);
   out->clock_mhz = d.clk_ref_ticks > 0 ? d.clk_ticks / d.clk_ref_ticks * 100.0 : 0.0;
   out->host_cpu_ms = cpu - d.worker_cpu0_ms;
   out->host_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d.stats_t0).count();
   out->dead = d.dead ? 1 : 0;
-  out->pool_groups = pool_shape(d).lockstep ? pool_shape(d).groups : 0;
+  out->pool_groups = kLsGroups;
   out->early_finishes = d.early;
   out->early_mismatches = d.early_mismatch;
   out->yields = d.yields;
   out->dyn_entries = d.dyn;
+  out->kills_relayed = d.kills_relayed;
+  return NPOW_OK;
+}
+
+// ABI 2 callers allocate the struct up to dyn_entries: never write past it here.
+int npow_device_stats_get(int device, npow_device_stats* out) try {
+  npow_device_stats full;
+  if (int rc = stats_fill(device, &full)) return rc;
+  memcpy(out, &full, offsetof(npow_device_stats, kills_relayed));
+  return NPOW_OK;
+} catch (...) { return guard_exception(); }
+
+int npow_device_stats_get_sized(int device, npow_device_stats* out, uint64_t size) try {
+  npow_device_stats full;
+  if (int rc = stats_fill(device, &full)) return rc;
+  memcpy(out, &full, std::min<uint64_t>(size, sizeof(full)));
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 
@@ -442,7 +447,7 @@ int npow_device_stats_reset(int device) try {
   settle_stats(d);
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
-  d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = 0;
+  d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = d.kills_relayed = 0;
   d.kernel_ms = 0.0;
   d.clk_ticks = d.clk_ref_ticks = 0.0;
   d.stats_t0 = std::chrono::steady_clock::now();
@@ -518,6 +523,20 @@ int npow_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce_out, uint64_t
   return pool_wait(ticket, timeout_us, nonce_out, value_out, nonces_done);
 } catch (...) { return guard_exception(); }
 
+int npow_wait_info(uint64_t ticket, int64_t timeout_us, npow_search_info* info) try {
+  if (int rc = check_init()) return rc;
+  if (!info || info->size < offsetof(npow_search_info, nonce))
+    return fail(NPOW_ERR_BAD_ARGUMENT, "info with info->size set is required");
+  npow_search_info full{};
+  full.size = (uint32_t)sizeof(full);
+  const int rc = pool_wait(ticket, timeout_us, &full.nonce, &full.value, &full.nonces_done, &full);
+  full.status = rc;
+  const uint32_t n = std::min<uint32_t>(info->size, (uint32_t)sizeof(full));
+  full.size = n;
+  memcpy(info, &full, n);
+  return rc;
+} catch (...) { return guard_exception(); }
+
 int npow_cancel(uint64_t ticket) try {
   if (int rc = check_init()) return rc;
   return pool_cancel(ticket);
@@ -582,7 +601,9 @@ int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint6
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 
-int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t count, uint64_t* values_out) try {
+// Values of [start, start + count) through one hash path (npow_values / npow_values_path).
+static int values_on(int device, const uint8_t root[32], uint64_t start, uint64_t count, Mode mode,
+                     uint64_t* values_out) {
   if (int rc = check_init()) return rc;
   if (device < 0 || device >= (int)g_devs.size() || !root || (count && !values_out))
     return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
@@ -598,7 +619,7 @@ int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t cou
     const uint64_t cnt = std::min(kValuesChunk, count - off);
     a.base = start + off;
     a.count = cnt;
-    rc = launch_chunk(d, Mode::kValues, a, 0, d.d_out);
+    rc = launch_chunk(d, mode, a, 0, d.d_out);
     if (rc) return rc;
     HIPTRY(hipMemcpyAsync(values_out + off, d.d_out, cnt * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
     HIPTRY(hipStreamSynchronize(d.stream));
@@ -606,6 +627,27 @@ int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t cou
   }
   DevState hs;
   return read_state(d, &hs);
+}
+
+int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t count, uint64_t* values_out) try {
+  return values_on(device, root, start, count, Mode::kValues, values_out);
+} catch (...) { return guard_exception(); }
+
+int npow_values_path(int device, const uint8_t root[32], uint64_t start, uint64_t count, int path,
+                     uint64_t* values_out) try {
+  if (path == NPOW_PATH_SEARCH) return values_on(device, root, start, count, Mode::kValues, values_out);
+  if (path == NPOW_PATH_SEQ) return values_on(device, root, start, count, Mode::kValuesSeq, values_out);
+  if (path == NPOW_PATH_GENERIC) {
+    if (count > 0xffffffffull) return fail(NPOW_ERR_BAD_ARGUMENT, "generic path: count must be < 2^32");
+    std::vector<uint8_t> roots((size_t)count * 32);
+    std::vector<uint64_t> nonces((size_t)count);
+    for (uint64_t i = 0; i < count; ++i) {
+      memcpy(&roots[(size_t)i * 32], root, 32);
+      nonces[(size_t)i] = start + i;
+    }
+    return npow_values_pairs(device, roots.data(), nonces.data(), (uint32_t)count, values_out);
+  }
+  return fail(NPOW_ERR_BAD_ARGUMENT, "path must be NPOW_PATH_SEARCH, NPOW_PATH_SEQ or NPOW_PATH_GENERIC");
 } catch (...) { return guard_exception(); }
 
 int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, uint32_t n, uint64_t* values_out) try {

@@ -58,6 +58,7 @@ struct Device {
   uint64_t launches = 0, nonces = 0, invalid = 0;
   uint64_t early = 0, early_mismatch = 0;  // jobs finished from a published final count (npow_pool.cpp)
   uint64_t yields = 0, dyn = 0;            // launches yielded / jobs that joined a running launch
+  uint64_t kills_relayed = 0;              // losing jobs stopped by another device's decision (npow_pool.cpp)
   // Published by the pool worker for npow_device_stats_get: it has launches or slots in flight, and
   // how many of its slots are still searching.  A job finished early returns before the launch that
   // held it is retired; with no slot searching, the stats wait for the worker to retire the rest.
@@ -77,20 +78,13 @@ struct Device {
 extern std::vector<std::unique_ptr<Device>> g_devs;
 extern std::atomic<uint32_t> g_iters;          // wave iterations per launch
 extern std::atomic<uint32_t> g_poll;           // host-word poll interval (iterations per wave)
-extern std::atomic<uint32_t> g_blocks_per_cu;  // workgroups per CU
+extern std::atomic<uint32_t> g_blocks_per_cu;  // npow_values_kernel_seq: 256-lane workgroups per CU
 extern std::atomic<uint32_t> g_budget_us;      // pool launches: wall-clock budget per wave (0 = off)
-extern std::atomic<uint32_t> g_pool_blocks_per_cu;  // pool launches: workgroups per CU
 
-inline int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }        // sweep / values
-// Search launches: the lockstep kernel (default) with one 1,024-lane workgroup per CU, or the
-// seq kernel with g_pool_blocks_per_cu 256-lane workgroups per CU (NANOPOW_POOL_KERNEL=seq).
-extern bool g_pool_lockstep;
-extern uint32_t g_ls_lds;     // lockstep: dynamic LDS bytes per workgroup (NANOPOW_LS_LDS)
-extern int g_ls_groups;       // lockstep: workgroups per CU, 1 or 2 (NANOPOW_LS_GROUPS)
-inline PoolShape pool_shape(const Device& d) {
-  if (g_pool_lockstep) return PoolShape{true, d.cus * g_ls_groups, g_ls_lds, g_ls_groups};
-  return PoolShape{false, d.cus * (int)g_pool_blocks_per_cu.load(), 0, 1};
-}
+inline int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }  // npow_values_kernel_seq
+// Search, sweep and values launches of the shipped stream: kLsGroups 1,024-lane workgroups per CU.
+inline int ls_grid(const Device& d) { return d.cus * kLsGroups; }
+inline PoolShape pool_shape(const Device& d) { return PoolShape{ls_grid(d)}; }
 inline uint32_t poll_mask() {
   uint32_t p = g_poll.load();
   uint32_t m = 1;
@@ -134,6 +128,7 @@ std::vector<Device*> select_devices(uint64_t mask);
 void account_launch(Device& d, int ring);
 
 // ---- work pool (npow_pool.cpp) ----------------------------------------------------------------
+bool test_hooks_enabled();          // NANOPOW_TEST_HOOKS=1: the NANOPOW_FAULT_* hooks are honoured
 int pool_device_init(Device& d);     // allocate pool buffers of one device
 void pool_device_free(Device& d);
 void pool_start();                   // start one worker thread per device
@@ -141,7 +136,9 @@ void pool_stop();                    // stop and join the workers (pending jobs 
 void pool_exit();                    // process exit: join the workers without further HIP calls
 int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
                 uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket);
-int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done);
+// info (may be null): the search's timeline and overshoot (npow_wait_info)
+int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done,
+              npow_search_info* info = nullptr);
 int pool_cancel(uint64_t ticket);
 int pool_set_max_active(uint32_t n);
 void pool_counts(uint32_t* queued, uint32_t* active);

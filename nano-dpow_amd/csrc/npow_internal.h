@@ -6,18 +6,19 @@
 
 #include "npow_blake2b.h"
 #include "npow_hash_asm.inc"
-#include "npow_hash_asm_lockstep.inc"
 #include "npow_hash_asm_lockstep_ld.inc"
 
 namespace npow {
 
-constexpr int kBlock = 256;  // lanes per workgroup (4 waves of 64)
-constexpr int kLsWaves = 16;                // lockstep pool kernel: waves per workgroup (4 per SIMD) ...
-constexpr int kLsBlock = kLsWaves * 64;     // ... one workgroup per CU
+constexpr int kBlock = 256;               // npow_values_kernel_seq / npow_pairs_kernel: lanes per workgroup
+constexpr int kLsWaves = 16;              // lockstep kernels: waves per workgroup (4 per SIMD) ...
+constexpr int kLsBlock = kLsWaves * 64;   // ... 1,024 lanes
+constexpr int kLsGroups = 2;              // ... two workgroups per CU: 8 waves per SIMD, 64 VGPRs each
 
-// npow_task_kernel (kSweep, kValues) / npow_sweep_kernel_ls (kSweepLs: one 1,024-lane workgroup
-// per CU); first-win searches: npow_pool_kernel*
-enum class Mode : int { kSweep = 1, kValues = 2, kSweepLs = 3, kSweepLs2 = 4 };  // Ls2: two workgroups per CU
+// One-root tasks (launch_task): npow_sweep_kernel_ls2 (kSweep), npow_values_kernel_ls2 (kValues, the
+// shipped stream), npow_values_kernel_seq (kValuesSeq, the second stream); first-win searches are
+// the pool's (npow_pool_kernel_ls2*).
+enum class Mode : int { kSweep = 1, kValues = 2, kValuesSeq = 3 };
 
 // Kernel arguments, passed by value: the kernarg segment lands in SGPRs, so the
 // root-derived uniforms and the threshold cost no memory traffic per nonce
@@ -38,7 +39,7 @@ struct LaunchArgs {
 // count once at exit, and 8,192 waves adding to ONE word serialise at the memory
 // side (~12 ns each, MI355X_MICROARCH.md "fanin") -- a ~100 us tail on every launch.
 constexpr int kDoneShards = 256;
-constexpr int kClaimRanges = 8;  // sweep sub-ranges per launch (one per XCD), npow_task_kernel
+constexpr int kClaimRanges = 8;  // sweep sub-ranges per launch (one per XCD), npow_sweep_kernel_ls2
 struct DevState {
   union {
     struct {
@@ -53,7 +54,7 @@ struct DevState {
   uint64_t value;           // winning value (search)
   uint32_t zero;            // always 0: the non-polling iterations' load target
   uint8_t pad1[64 - 36];
-  // Sweep work counters (64-nonce wave iterations claimed so far) of the launch's 8 sub-ranges
+  // Sweep work counters (rows of 16 blocks claimed so far) of the launch's 8 sub-ranges
   // (one per XCD), for each launch parity: launch k claims from claim[k & 1][*] and zeroes
   // claim[(k + 1) & 1][*] for launch k + 1 (same stream, so launch k - 1, their previous
   // user, has finished).  One cache line each: atomics on one address serialise (~18 ns
@@ -81,23 +82,24 @@ struct alignas(64) HostMailbox {
   uint8_t pad2[60];
 };
 
-// ---- Work pool: many roots searched by one launch (npow_pool_kernel) -----------------------
+// ---- Work pool: many roots searched by one launch (npow_pool_kernel_ls2*) -------------------
 // Each device keeps up to kMaxSlots live jobs in "slots".  Every launch reads a table of
-// the live entries (device memory, one copy per in-flight launch); wave w starts on entry
-// w % n.  A slot is identified per job by a generation number `gen` (unique, > 0): a slot
+// the live entries (its kernel arguments, or device memory past kArgEntries entries);
+// workgroup g starts on entry g % n.  A slot is identified per job by a generation number `gen` (unique, > 0): a slot
 // is dead for generation g once PoolDevState::slot[s].dead >= g (set by its winner with
 // atomicMax, or relayed from the host kill word), so a slot can be reused for a new job
 // with a larger gen without clearing any device memory.
 constexpr int kMaxSlots = 64;
 constexpr int kPoolDoneShards = 32;
 
-// Nonce-index mapping of one entry (the launch's region is [base, base + count)):
+// Nonce-index mapping of one entry (the launch's region is [base, base + count)); w = g * 16 + wave:
 //  * unbounded (search until won/cancelled): index = (it * W + w) * 64 + lane, W = grid
-//    waves -- every (iteration, wave) pair is distinct, so waves that migrate here from a
+//    waves -- every (iteration, wave) pair is distinct, so workgroups that move here from a
 //    dead entry hash fresh nonces; the region spans W * iters * 64 nonces (holes allowed);
 //  * bounded (max_nonces set; must cover its range exactly once): only the entry's own
-//    waves (w % n == e, rank j = w / n, k_e of them) run it, index = (it * k_e + j) * 64 +
-//    lane, dense over [0, count) with count <= k_e * iters * 64; migrants never enter it.
+//    workgroups (g % n == e, rank r = g / n, k_e of them) run it, index = (it * 16 k_e + 16 r +
+//    wave) * 64 + lane, dense over [0, count) with count <= 16 k_e * iters * 64; others never
+//    enter it.
 struct PoolEntry {
   uint64_t u[NPOW_ASM_N_UNIFORMS];  // nonce-independent intermediates of the root
   uint64_t threshold;
@@ -105,7 +107,7 @@ struct PoolEntry {
   uint64_t count;
   uint64_t gen;
   uint32_t slot;     // device slot index (PoolDevState / PoolMailbox arrays)
-  uint32_t bounded;  // 1: dense mapping over the entry's own waves, no migrants
+  uint32_t bounded;  // 1: dense mapping over the entry's own workgroups, no migrants
 };
 static_assert(offsetof(PoolEntry, u) == 0, "the two-group kernel finds an entry from its uniforms' address");
 struct PoolTable {
@@ -208,37 +210,33 @@ struct PoolMailbox {
   alignas(64) PoolClk clk[4][kClkWaves];  // [launch ring][XCD] (host: kEventRing == 4)
 };
 
-// Grid of a search launch.  A "unit" is what an entry's share is counted in: a wave (seq kernel)
-// or a workgroup of kLsWaves waves (lockstep kernel, whose workgroups work on one entry at a time).
+// Grid of a search launch: kLsGroups 1,024-lane workgroups per CU.  A "unit" is what an entry's share
+// is counted in: a workgroup of kLsWaves waves (workgroups work on one entry at a time).
 struct PoolShape {
-  bool lockstep;  // npow_pool_kernel_ls* (1,024-lane workgroups) instead of npow_pool_kernel*
-  int grid;       // workgroups
-  uint32_t lds;   // lockstep: dynamic LDS bytes per workgroup (> half a CU's keeps one per CU)
-  int groups;     // lockstep: workgroups per CU (2: npow_pool_kernel_ls2*, 8 waves per SIMD)
-  uint32_t units() const { return lockstep ? (uint32_t)grid : (uint32_t)grid * (kBlock / 64); }
-  uint32_t waves_per_unit() const { return lockstep ? (uint32_t)kLsWaves : 1u; }
+  int grid;  // workgroups
+  uint32_t units() const { return (uint32_t)grid; }
   // nonces a bounded entry e of n can cover in one launch of `iters` wave iterations
   uint64_t own(uint32_t e, uint32_t n, uint32_t iters) const {
     const uint32_t U = units();
-    return (uint64_t)(U / n + (e < U % n ? 1u : 0u)) * waves_per_unit() * iters * 64;
+    return (uint64_t)(U / n + (e < U % n ? 1u : 0u)) * kLsWaves * iters * 64;
   }
-  uint64_t full(uint32_t iters) const { return (uint64_t)units() * waves_per_unit() * iters * 64; }
-  // The iteration cap of a launch: with two lockstep workgroups per CU a wave iteration takes
-  // twice as long, so half the cap keeps a launch's longest duration (and its nonce span) unchanged.
-  uint32_t launch_iters(uint32_t iters) const {
-    return lockstep && groups == 2 ? (iters > 1 ? iters / 2 : 1u) : iters;
-  }
+  uint64_t full(uint32_t iters) const { return (uint64_t)units() * kLsWaves * iters * 64; }
+  // The iteration cap of a launch: with two lockstep workgroups per CU a wave iteration takes as long
+  // as two hashes of its SIMD's other group, so half of g_iters keeps a launch's longest duration
+  // (and its nonce span) where the round-1 tuning put it.
+  uint32_t launch_iters(uint32_t iters) const { return iters > 1 ? iters / 2 : 1u; }
 };
 
 // Launchers (defined in npow_kernel.hip).
 hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs& a, DevState* st,
                        HostMailbox* mb, uint64_t* out);
-// bounded: the table holds a bounded entry (selects the kernel variant with per-lane range tests)
-hipError_t launch_pool(const PoolShape& sh, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
+// bounded: the table holds a bounded entry (selects the kernel variant with per-lane range tests);
+// the table in device memory (more than kArgEntries entries, uploaded in stream order before it)
+hipError_t launch_pool(hipStream_t stream, int grid, const PoolTable* tab, bool bounded, PoolDevState* st,
                        PoolMailbox* mb);
 // The same with the table (n <= kArgEntries) passed in the kernel arguments: no upload.
-hipError_t launch_pool_arg(const PoolShape& sh, hipStream_t stream, const PoolTable& host_tab, bool bounded,
-                           PoolDevState* st, PoolMailbox* mb);
+hipError_t launch_pool_arg(hipStream_t stream, int grid, const PoolTable& host_tab, bool bounded, PoolDevState* st,
+                           PoolMailbox* mb);
 // Fill a.u[] for one root (host).
 inline void fill_uniforms(LaunchArgs& a, const RootPrecomp& pre) { npow_asm_uniforms(pre.m, a.u); }
 

@@ -4,33 +4,30 @@
 // reference work server (client/bin/windows/nano-work-server.exe @1657474..1661900).
 // Written from the BLAKE2b definition for the gfx950 VALU, not translated:
 //
-//  * The per-nonce hash is the generated instruction stream npow_hash_asm.inc
-//    (tools/gen_hash_asm.py): one nonce per lane, the 16-word state in a fixed
-//    VGPR window, 12 rounds unrolled with the message schedule resolved at
-//    generation time (11 of 16 message words are zero).  Every nonce-independent
-//    intermediate (round 1's three column steps and more) is computed once per
-//    root on the host and arrives in SGPRs.  Round 12's dead half is removed.
-//  * 64-bit adds are single `v_lshl_add_u64` instructions (half rate, 4 SIMD cycles
-//    for the whole add; the v_add_co/v_addc carry pair serialises the wave on VCC --
-//    DESIGN.md section 4, profiles/r01_valu_mix2_timebudget.jsonl).
-//  * Rotations are split into 32-bit halves: rotr32 is a free register swap
-//    folded into the xor that feeds it, rotr24 / rotr16 are two `v_alignbit_b32`,
-//    rotr63 is `v_lshrrev_b32` + `v_lshl_add_u64 x, 1, {hi >> 31, 0}`.
-//  * The hit test is a wave ballot, so a wave leaves the fast path only when one of
-//    its 64 lanes wins.
-//  * Lockstep kernels (default; npow_pool_kernel_ls*, npow_sweep_kernel_ls): the same hash
-//    as npow_hash_asm_lockstep.inc, scheduled in barrier-separated intervals, run by one
-//    1,024-lane workgroup per CU whose waves stay in the same phase;
-//    every loop decision is a workgroup decision.  The kernels below are their seq forms.
-//  * First-win search (npow_pool_kernel): every live job of the device's work
-//    pool in one launch; first win per job by atomicMax on its slot's dead word,
-//    published to a host-coherent mailbox with system-scope stores; every wave
-//    polls its slot's dead word each iteration (agent-scope load, L2) and the
-//    host kill / yield words every poll_mask+1 iterations (system-scope loads); a
-//    launch ends on a wall-clock budget read from s_memrealtime.
-//  * Sweep (npow_task_kernel<kSweep>): waves claim runs of iterations from 8
-//    per-XCD counters; every hit appended through an atomic counter (order-free;
-//    the host sorts).  Values mode: grid-stride, writes every value (parity tests).
+//  * The per-nonce hash is a generated instruction stream (tools/gen_hash_asm.py): one nonce per
+//    lane, the 16-word state in a fixed VGPR window, 12 rounds unrolled with the message schedule
+//    resolved at generation time (11 of 16 message words are zero).  Every nonce-independent
+//    intermediate (round 1's three column steps and more) is computed once per root on the host.
+//    Round 12's dead half is removed.
+//  * 64-bit adds are single `v_lshl_add_u64` instructions (half rate, 4 SIMD cycles for the whole
+//    add; the v_add_co/v_addc carry pair serialises the wave on VCC -- DESIGN.md section 4).
+//  * Rotations are split into 32-bit halves: rotr32 is a free register swap folded into the xor
+//    that feeds it, rotr24 / rotr16 are two `v_alignbit_b32`, rotr63 is `v_lshrrev_b32` +
+//    `v_lshl_add_u64 x, 1, {hi >> 31, 0}`.
+//  * The shipped stream, npow_hash_asm_lockstep_ld.inc, is scheduled in barrier-separated
+//    intervals (the full-rate part of one G step, then the half-rate part of the next) and loads
+//    the root's uniforms into SGPRs itself.  Every kernel that runs it (search, sweep, values) has
+//    two 1,024-lane workgroups per CU whose waves stay in phase, so every
+//    loop decision is a workgroup decision.
+//  * First-win search (npow_pool_kernel_ls2*): every live job of the device's work pool in one
+//    launch; first win per job by atomicMax on its slot's dead word, published to a host-coherent
+//    mailbox with system-scope stores; the host kill / yield words are polled by one wave in
+//    poll_mask+1 per iteration; a launch ends on a wall-clock budget read from s_memrealtime.
+//  * Sweep (npow_sweep_kernel_ls2): workgroups claim rows of blocks from 8 per-XCD counters; every
+//    hit appended through an atomic counter (order-free; the host sorts).
+//  * Values (npow_values_kernel_ls2): every value of a range through the same stream (parity); a
+//    second, independently scheduled stream (npow_hash_asm.inc, no barriers) backs
+//    npow_values_kernel_seq, and npow_pairs_kernel is plain C++ (per-lane roots).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string.h>
@@ -117,172 +114,48 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t x, int lane) {
   return pack(lo, hi);
 }
 
-template <Mode MODE>
-__global__ __launch_bounds__(kBlock) void npow_task_kernel(const LaunchArgs a, DevState* __restrict__ st,
-                                                             HostMailbox* __restrict__ mb,
-                                                             uint64_t* __restrict__ out) {
-  // Uniform copies (the compiler keeps kernel arguments in SGPRs).
-  uint64_t u[NPOW_ASM_N_UNIFORMS];
+// ---- Values through the seq stream (npow_values_kernel_seq) ---------------------------------
+// The second hash path: npow_hash_asm.inc (the same DAG, list-scheduled without barriers, uniforms
+// as asm operands), 256-lane workgroups, static grid-stride mapping.
+__global__ __launch_bounds__(kBlock) void npow_values_kernel_seq(const LaunchArgs a, DevState* __restrict__ st,
+                                                                 uint64_t* __restrict__ out) {
+  uint64_t u[NPOW_ASM_N_UNIFORMS];  // the compiler keeps kernel arguments in SGPRs
 #pragma unroll
   for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) u[i] = a.u[i];
-
   const uint32_t lane = threadIdx.x & 63;
-  // First lane index of this wave; wave-uniform.
-  const uint64_t wave0 =
-      (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kBlock + (threadIdx.x & ~63u));
-  const uint32_t wave_id = (uint32_t)(wave0 >> 6);
-  uint64_t done = 0;  // nonces this wave hashed (wave-uniform)
-  uint32_t iter = 0;
-
-  // One 64-nonce wave iteration at lane offset ib; false = stop (abort / stop word).
-  auto step = [&](uint64_t ib) -> bool {
-    // Early-exit polls:
-    //  * every iteration, one agent-scope (L2) load of the device stop word
-    //    {found, abort} -- relayed from the host; it is issued first and consumed after
-    //    the hash, so its latency is hidden;
-    //  * the host abort word lives in pinned host memory (a PCIe read whose latency and
-    //    throughput vary by host), so only one wave in poll_mask+1 reads it per iteration
-    //    (staggered by wave id) and relays a raised abort into the device stop word.
-    uint64_t stop_word = 0;
-    uint32_t host_abort = 0;
-    if constexpr (MODE != Mode::kValues) {
-      stop_word = __hip_atomic_load(&st->stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (((iter + wave_id) & a.poll_mask) == 0)
-        host_abort = __hip_atomic_load(&mb->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    ++iter;
+  const uint64_t wave0 = (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x * kBlock + (threadIdx.x & ~63u));
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  uint64_t done = 0;
+  for (uint64_t ib = wave0; ib < a.count; ib += stride) {
     const uint64_t i = ib + lane;
-    const uint64_t nonce = a.base + i;
-    const uint64_t value = npow_asm_work_value(nonce, u);
-    const bool in_range = i < a.count;
+    const uint64_t value = npow_asm_work_value(a.base + i, u);
+    if (i < a.count) out[i] = value;
     const uint64_t rem = a.count - ib;
     done += rem < 64 ? rem : 64;
-
-    if constexpr (MODE == Mode::kValues) {
-      if (in_range) out[i] = value;
-    } else {
-      const bool hit = in_range && value >= a.threshold;
-      const uint64_t hits = __ballot(hit);
-      if (__builtin_expect(hits != 0, 0) && hit) {  // sweep: append every hit
-        const uint32_t slot = atomicAdd(&st->n_hits, 1u);
-        if (slot < a.cap) out[slot] = nonce;
-      }
-      if (__builtin_amdgcn_readfirstlane(host_abort)) {
-        if (lane == 0) __hip_atomic_store(&st->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return false;
-      }
-      if (__builtin_amdgcn_readfirstlane((uint32_t)stop_word | (uint32_t)(stop_word >> 32))) return false;
-    }
-    return true;
-  };
-
-  if constexpr (MODE == Mode::kValues) {
-    // Static grid-stride mapping (parity tests: no hits, no early exit).
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    for (uint64_t ib = wave0; ib < a.count; ib += stride) step(ib);
-  } else {
-    // Sweep: waves claim runs of 64-nonce iterations from counters instead of owning a fixed
-    // share.  VALU issue favours a SIMD's oldest wave, so with fixed shares the young waves
-    // finish late and the launch ends in a tail with one or two waves per SIMD; claiming keeps
-    // every SIMD full until the range is used up.  The launch's T iterations are split into 8
-    // sub-ranges with one counter each (atomics on ONE address serialise at ~18 ns: 8,192 waves
-    // claiming 8 iterations at a time halve the throughput); a wave starts on its XCD's
-    // sub-range (workgroups are dealt to XCDs round-robin) and then helps the others.  Claim
-    // size = remaining / (2 x waves per sub-range), between 1 and max_claim (guided
-    // self-scheduling, capped because a young wave is several times slower than an old one).
-    //
-    // The inner loop keeps its bookkeeping scalar: 32-bit iteration indices (a launch is at most
-    // 2^37 nonces, engine: 2^31), the per-lane range test only in the launch's last block, the
-    // host abort word loaded and tested only by polling waves, and the device stop word read as
-    // its 32-bit abort half (found is unused): besides the hash, an iteration issues the nonce
-    // add, the threshold compare and one v_readfirstlane (11 VALU instructions before).
-    const uint32_t slot = a.claim_slot & 1;
-    if (blockIdx.x == 0 && threadIdx.x < kClaimRanges)
-      __hip_atomic_store(&st->claim[((1 - slot) * kClaimRanges + threadIdx.x) * 8], 0ull, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t T = (uint32_t)((a.count + 63) >> 6);                      // wave iterations
-    const uint32_t last_lanes = (uint32_t)(a.count - ((uint64_t)(T - 1) << 6));  // 1..64 in block T-1
-    const uint64_t W2 = 2ull * gridDim.x * (kBlock / 64) / kClaimRanges;     // 2 x waves per sub-range
-    const uint64_t lane_nonce = a.base + lane;                               // + block * 64
-    const uint32_t home = blockIdx.x % kClaimRanges;
-    bool go = true;
-    for (uint32_t k = 0; k < kClaimRanges && go; ++k) {
-      const uint32_t x = (home + k) % kClaimRanges;
-      const uint32_t lo = (uint32_t)((uint64_t)T * x / kClaimRanges);
-      const uint32_t Tx = (uint32_t)((uint64_t)T * (x + 1) / kClaimRanges) - lo;
-      unsigned long long* ctr = &st->claim[(slot * kClaimRanges + x) * 8];
-      uint64_t seen = 0;  // the counter as last seen by this wave
-      if (k) {            // helping: start from the counter's current value (it may be nearly used up)
-        uint64_t cur = 0;
-        if (lane == 0) cur = __hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        seen = readlane64(cur, 0);
-      }
-      while (go && seen < Tx) {
-        uint64_t n = (Tx - seen) / W2;
-        n = n < 1 ? 1 : (n > a.max_claim ? a.max_claim : n);
-        uint64_t c = 0;
-        if (lane == 0) c = atomicAdd(ctr, (unsigned long long)n);
-        c = readlane64(c, 0);
-        if (c >= Tx) break;
-        seen = c + n;
-        const uint32_t end = lo + (uint32_t)(seen < Tx ? seen : Tx);
-        for (uint32_t blk = lo + (uint32_t)c; blk < end; ++blk) {
-          // polls, issued before the hash and consumed after it (see step() above)
-          const uint32_t stop = __hip_atomic_load(&st->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          const bool poll = ((iter + wave_id) & a.poll_mask) == 0;  // wave-uniform
-          uint32_t host_abort;
-          if (__builtin_expect(poll, 0))
-            host_abort = __hip_atomic_load(&mb->abort, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          ++iter;
-          const uint64_t nonce = lane_nonce + ((uint64_t)blk << 6);
-          const uint64_t value = npow_asm_work_value(nonce, u);
-          uint64_t hits = __ballot(value >= a.threshold);  // the compare writes the mask directly
-          if (__builtin_expect(blk == T - 1, 0)) {        // the launch's last block may be partial
-            hits &= last_lanes == 64 ? ~0ull : (1ull << last_lanes) - 1;
-            done += last_lanes;
-          } else {
-            done += 64;
-          }
-          if (__builtin_expect(hits != 0, 0) && ((hits >> lane) & 1)) {  // append every hit
-            const uint32_t hs = atomicAdd(&st->n_hits, 1u);
-            if (hs < a.cap) out[hs] = nonce;
-          }
-          if (__builtin_expect(poll, 0) && __builtin_amdgcn_readfirstlane(host_abort)) {
-            if (lane == 0) __hip_atomic_store(&st->abort, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            go = false;
-            break;
-          }
-          if (__builtin_amdgcn_readfirstlane(stop)) {
-            go = false;
-            break;
-          }
-        }
-      }
-    }
   }
   if (lane == 0 && done) atomicAdd(&st->done_shard[(blockIdx.x % kDoneShards) * 8], (unsigned long long)done);
 }
 
-// ---- Lockstep sweep (npow_sweep_kernel_ls) -------------------------------------------------
-// npow_task_kernel<kSweep> with the lockstep stream (pool_body_ls): 1,024-lane workgroups, one
-// per CU, so everything that shapes a wave's loop is per workgroup.  The unit of work is a row of
+// ---- Sweep (npow_sweep_kernel_ls2) -----------------------------------------------------------
+// Every hit of [base, base + count): two 1,024-lane workgroups per CU.  The unit of work is a row of
 // 16 consecutive 64-nonce blocks, one per wave (block = row * 16 + wave); workgroups claim runs of
-// rows from the same 8 per-XCD counters (thread 0 claims and LDS broadcasts the claim: two
-// barriers per claim of <= max_claim rows), and the stop words (the device abort word, and the
-// pinned host abort word on one claim in poll_mask + 1) are read with the claim, so a cancel
-// lands within one claim (<= 64 rows, ~0.15 ms).  Blocks past the range's end are masked off.
-template <bool LD>
-__device__ __forceinline__ void sweep_body_ls(const LaunchArgs& a, DevState* __restrict__ st,
-                                              HostMailbox* __restrict__ mb, uint64_t* __restrict__ out) {
+// rows from 8 per-XCD counters (thread 0 claims and LDS broadcasts the claim: two barriers per claim
+// of <= max_claim rows), and the stop words (the device abort word, and the pinned host abort word on
+// one claim in poll_mask + 1) are read with the claim, so a cancel lands within one claim (<= 64
+// rows, ~0.15 ms).  Blocks past the range's end are masked off.
+//
+// Why claims: VALU issue favours a SIMD's oldest wave, so with fixed shares the
+// young workgroups finish late and the launch ends in a tail; claiming keeps every SIMD full until
+// the range is used up.  The launch's rows are split into 8 sub-ranges with one counter each on its
+// own cache line (atomics on ONE address serialise at ~18 ns); a workgroup starts on its XCD's
+// sub-range (workgroups are dealt to XCDs round-robin) and then helps the others.  Claim size =
+// remaining / (2 x workgroups per sub-range), between 1 and max_claim.  The counters alternate by
+// launch parity: launch k claims from claim[k & 1][*] and zeroes claim[(k + 1) & 1][*].
+__global__ __launch_bounds__(kLsBlock, 8) void npow_sweep_kernel_ls2(const LaunchArgs a, DevState* __restrict__ st,
+                                                                    HostMailbox* __restrict__ mb,
+                                                                    uint64_t* __restrict__ out) {
   __shared__ uint32_t s_claim[3];  // first row, end row (within the sub-range), stop
-  uint64_t u[NPOW_ASM_N_UNIFORMS];
-  const uint64_t* up = nullptr;  // LD: the uniforms in the kernel arguments, loaded by the stream
-  if constexpr (LD) {
-    up = ((const LaunchArgs*)__builtin_amdgcn_kernarg_segment_ptr())->u;
-  } else {
-#pragma unroll
-    for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) u[i] = a.u[i];
-  }
+  const uint64_t* up = ((const LaunchArgs*)__builtin_amdgcn_kernarg_segment_ptr())->u;  // loaded by the stream
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t g = blockIdx.x;
@@ -343,11 +216,7 @@ __device__ __forceinline__ void sweep_body_ls(const LaunchArgs& a, DevState* __r
       for (uint32_t row = lo + c; row < lo + end; ++row) {
         const uint32_t b = row * kLsWaves + wv;
         const uint64_t nonce = lane_nonce + ((uint64_t)b << 6);
-        uint64_t value;
-        if constexpr (LD)
-          value = npow_asm_work_value_lockstep_ld(nonce, up);
-        else
-          value = npow_asm_work_value_lockstep(nonce, u);
+        const uint64_t value = npow_asm_work_value_lockstep_ld(nonce, up);
         uint64_t hits = __ballot(value >= a.threshold);
         if (__builtin_expect(b >= T - 1, 0)) {  // the last block may be partial; blocks past it are empty
           const uint32_t nl = b == T - 1 ? last_lanes : 0u;
@@ -367,33 +236,42 @@ __device__ __forceinline__ void sweep_body_ls(const LaunchArgs& a, DevState* __r
     atomicAdd(&st->done_shard[((g * kLsWaves + wv) % kDoneShards) * 8], (unsigned long long)done);
 }
 
-__global__ __launch_bounds__(kLsBlock) void npow_sweep_kernel_ls(const LaunchArgs a, DevState* __restrict__ st,
-                                                                HostMailbox* __restrict__ mb,
-                                                                uint64_t* __restrict__ out) {
-  sweep_body_ls<false>(a, st, mb, out);
+// ---- Values through the shipped stream (npow_values_kernel_ls2) ----------------------------------
+// Every value of [base, base + count), hashed by exactly the instruction stream the search and sweep
+// kernels run (npow_hash_asm_lockstep_ld.inc: the same uniform loads, the same barrier intervals, the
+// same two-workgroups-per-CU shape), so the parity tests compare that stream's 64-bit values with the
+// oracle -- not only its hit / no-hit decisions.  Rows of 16 blocks (one per wave) go to workgroups
+// round-robin; every wave of a workgroup runs the same number of rows (the stream's barriers need
+// workgroup-uniform control flow), and lanes past the range's end hash but do not store.
+// 8 bytes per nonce written (the only kernel with algorithmic HBM traffic), coalesced: a wave stores
+// 512 contiguous bytes per row.
+__global__ __launch_bounds__(kLsBlock, 8) void npow_values_kernel_ls2(const LaunchArgs a, DevState* __restrict__ st,
+                                                                     uint64_t* __restrict__ out) {
+  const uint64_t* up = ((const LaunchArgs*)__builtin_amdgcn_kernarg_segment_ptr())->u;  // loaded by the stream
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t T = (uint32_t)((a.count + 63) >> 6);   // 64-nonce blocks (count <= 2^31 per launch)
+  const uint32_t R = (T + kLsWaves - 1) / kLsWaves;     // rows
+  uint64_t done = 0;
+  for (uint32_t row = blockIdx.x; row < R; row += gridDim.x) {  // workgroup-uniform
+    const uint32_t b = row * kLsWaves + wv;
+    const uint64_t i = ((uint64_t)b << 6) + lane;
+    const uint64_t value = npow_asm_work_value_lockstep_ld(a.base + i, up);
+    if (i < a.count) out[i] = value;
+    const uint64_t first = (uint64_t)b << 6;
+    done += first >= a.count ? 0 : (a.count - first < 64 ? a.count - first : 64);
+  }
+  if (lane == 0 && done)
+    atomicAdd(&st->done_shard[((blockIdx.x * kLsWaves + wv) % kDoneShards) * 8], (unsigned long long)done);
 }
 
-// Two lockstep workgroups per CU: 8 waves per SIMD (64 VGPRs, 80 SGPRs per wave).
-__global__ __launch_bounds__(kLsBlock, 8) void npow_sweep_kernel_ls2(const LaunchArgs a, DevState* __restrict__ st,
-                                                                    HostMailbox* __restrict__ mb,
-                                                                    uint64_t* __restrict__ out) {
-  sweep_body_ls<true>(a, st, mb, out);
-}
-
-// ---- Work pool: many roots per launch ------------------------------------------------------
-// One launch searches every live entry of the device's table (up to kMaxSlots jobs: the
-// DPoW burst, many work_generate requests in flight).  Wave w starts on entry w % n with
-// the entry's uniforms in SGPRs; when its entry dies (won here, won on another GPU,
-// cancelled, or its bounded range is used up) the wave moves to the next live unbounded
-// entry instead of idling for the rest of the launch.  Index mapping: PoolEntry comment in
-// npow_internal.h.  With one entry this is the plain first-win search.
-#ifdef NPOW_WAVE_PROBE
-__device__ uint64_t npow_wave_probe[32768 * 4];
-#endif
-
+// ---- Work pool: many roots per launch (npow_pool_kernel_ls2*) ----------------------------------
+// One launch searches every live entry of the device's table (up to kMaxSlots jobs: the DPoW
+// burst, many work_generate requests in flight) plus the dynamic entries published while it runs.
+// Index mapping: PoolEntry comment in npow_internal.h.  With one entry this is the plain first-win
+// search.
 struct PoolCursor {
-  uint64_t u[NPOW_ASM_N_UNIFORMS];
-  const uint64_t* up;  // the entry's uniforms in memory (lockstep LD kernels: the stream loads them)
+  const uint64_t* up;  // the entry's uniforms in memory (the stream loads them itself)
   uint64_t threshold, base, gen;
   uint32_t slot;
   uint32_t K, j;      // block index b = it * K + j; nonce = base + b * 64 + lane
@@ -403,195 +281,17 @@ struct PoolCursor {
   uint32_t bounded;   // exact dense coverage: ignores the launch's time budget
 };
 
-// Load entry `pe` into the cursor for wave w.  own: the entry's own waves (w % n == e) --
-// bounded entries are dense over their own waves; everything else uses (it, w) directly.
-__device__ __forceinline__ void pool_load(const PoolEntry* __restrict__ pe, PoolCursor& c, bool own, uint32_t w,
-                                          uint32_t W, uint32_t n, uint32_t e, uint32_t iters) {
-#pragma unroll
-  for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) c.u[i] = pe->u[i];
-  c.threshold = pe->threshold;
-  c.base = pe->base;
-  c.gen = pe->gen;
-  c.slot = pe->slot;
-  c.bounded = pe->bounded;
-  if (pe->bounded) {
-    // own waves only (migrants never pick a bounded entry); count <= K * iters * 64 < 2^32 * 64
-    c.K = W / n + (e < W % n ? 1u : 0u);
-    c.j = w / n;
-    const uint32_t blocks = (uint32_t)((pe->count + 63) / 64);  // <= K * iters < 2^31
-    c.it_end = blocks > c.j ? (blocks - c.j + c.K - 1) / c.K : 0u;
-    c.last_b = blocks - 1u;
-    c.tail = (uint32_t)(pe->count - (uint64_t)(blocks - 1u) * 64);
-  } else {
-    c.K = W;
-    c.j = w;
-    c.it_end = iters;
-    c.last_b = 0xffffffffu;
-    c.tail = 64;
-  }
-  (void)own;
-}
-
 __device__ __forceinline__ uint64_t load_dead(PoolDevState* st, uint32_t slot) {
   return __hip_atomic_load(&st->slot[slot].dead, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// BOUNDED: the table holds at least one bounded entry (partial last blocks need a per-lane
-// range test); the plain search (every entry unbounded) compiles without it.
-#ifndef NPOW_POOL_NUM_SGPR
-#define NPOW_POOL_NUM_SGPR 0
-#endif
-template <bool BOUNDED>
-__device__ __forceinline__ void pool_body(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
-                                          PoolMailbox* __restrict__ mb, const uint64_t t_start) {
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t w = __builtin_amdgcn_readfirstlane((blockIdx.x * kBlock + threadIdx.x) >> 6);
-  const uint32_t W = gridDim.x * (kBlock / 64);
-  const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask, budget = tab->budget;
-  const uint64_t yield_base = tab->yield_base >> 32;  // read once: the loop below compares against it
-  unsigned long long* const done_base = &st->done[0][(blockIdx.x % kPoolDoneShards) * 8];
-  // Time budget.  VALU issue on a SIMD goes to its OLDEST wave first (MI355X_MICROARCH.md:
-  // priority, then age), so the 8 waves of a SIMD do not progress together: the oldest runs
-  // at single-wave speed and finishes first, the youngest barely runs until the others are
-  // done (tools/experiments/wave_probe.cpp: wave finish times 1.0 - 5.6 ms in a 5.6-ms launch).  A launch
-  // of a fixed iteration count therefore ends in a tail where one or two waves per SIMD are
-  // left.  Unbounded entries need no fixed partition, so every wave instead stops at the same
-  // wall-clock point, its own start (read first thing, before any VALU instruction the age
-  // arbitration could hold back) + budget; region holes are unused nonces.
-
-  uint32_t e = w % n;
-  PoolCursor c;
-  pool_load(&tab->e[e], c, true, w, W, n, e, iters);
-
-  uint32_t it = 0;
-  bool out_of_time = false;
-  for (;;) {
-    uint32_t done = 0;  // nonces this wave hashed for the current entry (<= iters * 64)
-    while (it < c.it_end) {
-      // polls: the slot's dead word every iteration (agent scope, L2); the pinned host
-      // kill word by one wave in poll_mask+1 (a PCIe read).  Consumed after the hash.
-#ifndef NPOW_POOL_POLL
-#define NPOW_POOL_POLL 3
-#endif
-      // Only the hash, the nonce, the threshold compare and the dead compare are VALU work on
-      // the common path: the host words are loaded and compared only by polling waves, and the
-      // clock compare is scalar (a default value or a 64-bit compare here costs VALU issue).
-      const uint64_t dead = (NPOW_POOL_POLL & 1) ? load_dead(st, c.slot) : 0;
-      const bool poll = (NPOW_POOL_POLL & 2) && ((it + w) & poll_mask) == 0;  // wave-uniform
-      uint64_t kill, yld;
-      if (__builtin_expect(poll, 0)) {
-        kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        yld = __hip_atomic_load(&mb->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32;
-      }
-
-      const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;  // consumed after the hash
-      const uint32_t b = it * c.K + c.j;  // < 2^31: the entry's blocks of this launch
-      const uint64_t nonce = c.base + ((uint64_t)b << 6) + lane;
-      const uint64_t value = npow_asm_work_value(nonce, c.u);
-      ++it;
-      bool hit = value >= c.threshold;
-      if constexpr (BOUNDED) {
-        const uint32_t in_lanes = b == c.last_b ? c.tail : 64u;
-        hit = hit && lane < in_lanes;
-        done += in_lanes;
-      } else {
-        done += 64;
-      }
-      const uint64_t hits = __ballot(hit);
-      if (__builtin_expect(hits != 0, 0)) {
-        const int wl = __builtin_ctzll(hits);
-        const uint64_t wn = readlane64(nonce, wl), wv = readlane64(value, wl);
-        if (lane == 0) {
-          if (atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen) < c.gen) {  // first win
-            PoolWin* pw = &mb->win[c.slot];
-            __hip_atomic_store(&pw->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&pw->value, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&pw->gen, c.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-        }
-        break;
-      }
-      if (__builtin_expect(poll, 0)) {
-        if (readlane64(yld, 0) != yield_base) {
-          // the host has new jobs for this device: end every unbounded entry of this launch
-          // (their jobs come back in the next launch's table with new generations)
-          if (lane == 0)
-            for (uint32_t k = 0; k < n; ++k)
-              if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
-          if (!c.bounded) break;
-        }
-        if (readlane64(kill, 0) == c.gen) {  // generations only grow: == is "this job"
-          if (lane == 0) atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen);  // relay
-          break;
-        }
-      }
-      if (readlane64(dead, 0) == c.gen) break;
-      // out of time: the wave is done.  A 32-bit compare of the wrapped tick difference (s_cmp;
-      // a 64-bit one is a VALU v_cmp): exact while a launch lasts under 2^32 ticks = 42.9 s.
-      if (budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget) {
-        out_of_time = true;
-        break;
-      }
-    }
-    if (lane == 0 && done) atomicAdd(done_base + (size_t)c.slot * (kPoolDoneShards * 8), (unsigned long long)done);
-    if (it >= iters || out_of_time) break;
-    // the entry died or its bounded range is used up: next live unbounded entry (cyclic
-    // from e + 1); none left -> the wave is finished
-    uint32_t next = n;
-    for (uint32_t k = 1; k < n; ++k) {
-      uint32_t e2 = e + k;
-      if (e2 >= n) e2 -= n;
-      const PoolEntry* pe = &tab->e[e2];
-      if (pe->bounded) continue;
-      if (load_dead(st, pe->slot) >= pe->gen) continue;
-      next = e2;
-      break;
-    }
-    if (next == n) break;
-    e = next;
-    pool_load(&tab->e[e], c, false, w, W, n, e, iters);
-  }
-#ifdef NPOW_WAVE_PROBE
-  // diagnostic build (tools/experiments/wave_probe.cpp): per-wave start / end realtime, iterations, HW ids
-  if (lane == 0) {
-    npow_wave_probe[w * 4 + 0] = t_start;
-    npow_wave_probe[w * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-    npow_wave_probe[w * 4 + 2] = it;
-    npow_wave_probe[w * 4 + 3] = ((uint64_t)__builtin_amdgcn_s_getreg(20 | (31 << 11)) << 32) |  // XCC_ID
-                                 (uint32_t)__builtin_amdgcn_s_getreg(4 | (31 << 11));         // HW_ID
-  }
-#endif
-}
-
-// ---- Lockstep pool body (npow_pool_kernel_ls*) ---------------------------------------------
-// The same search with the lockstep instruction stream (npow_hash_asm_lockstep.inc): one
-// 1,024-lane workgroup per CU puts 4 waves on every SIMD, all of one workgroup, and the
-// stream's s_barrier after every interval (the full-rate part of one G step, then the
-// half-rate part of the next) keeps them in the same phase -- full-rate and half-rate runs of
-// different waves then no longer mix on the SIMD (5,251 vs 6,139 SIMD
-// cycles per hash in tools/experiments/stream_lockstep.py).  Every wave of a workgroup must
-// therefore hash the same number of times, so everything that ends a wave's loop is decided
-// per workgroup:
-//  * a workgroup works on one entry at a time (entry g % n first; bounded entries are dense
-//    over their own workgroups' waves, PoolEntry comment with unit = workgroup);
-//  * a wave that wants its workgroup to stop (a win, a dead / killed / yielded entry, the time
-//    budget) files a request in LDS, s_stop[segment % 3] = min((it + 1) << 1 | kind) with
-//    kind 0 = end the launch, 1 = leave the entry; every wave reads the word at the top of an
-//    iteration and obeys only requests filed at least one full hash earlier (value < it at the
-//    top): those lie behind the hash's barriers for every wave, so all waves reach the same
-//    verdict in the same iteration (two iterations after the request, ~4 us);
-//  * leaving an entry: wave 0 picks the next live unbounded entry and broadcasts it through
-//    LDS (one __syncthreads); each entry segment has its own request word (3 rotate: the word
-//    of segment s + 1 is reset at the end of segment s, after its last reader, segment s - 2).
-template <bool LD>
+// Load entry `pe` into the cursor of wave wv of workgroup g (G workgroups, n table entries, e =
+// this entry's index).  Bounded entries are dense over their own workgroups (g % n == e, rank
+// g / n); unbounded ones map (it, workgroup, wave) to distinct blocks, so a workgroup that moves
+// here from a dead entry hashes fresh nonces.
 __device__ __forceinline__ void pool_load_ls(const PoolEntry* __restrict__ pe, PoolCursor& c, uint32_t g, uint32_t wv,
                                              uint32_t G, uint32_t n, uint32_t e, uint32_t iters) {
-  if constexpr (LD) {
-    c.up = pe->u;
-  } else {
-#pragma unroll
-    for (int i = 0; i < NPOW_ASM_N_UNIFORMS; ++i) c.u[i] = pe->u[i];
-  }
+  c.up = pe->u;
   c.threshold = pe->threshold;
   c.base = pe->base;
   c.gen = pe->gen;
@@ -618,138 +318,10 @@ __device__ __forceinline__ void pool_load_ls(const PoolEntry* __restrict__ pe, P
 
 __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
-// LD: the stream loads the entry's uniforms itself (npow_hash_asm_lockstep_ld.inc), so the kernel
-// fits 8 waves per SIMD -- two lockstep workgroups per CU (npow_pool_kernel_ls2*).
-template <bool BOUNDED, bool LD>
-__device__ __forceinline__ void pool_body_ls(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
-                                             PoolMailbox* __restrict__ mb, const uint64_t t_start) {
-  __shared__ uint32_t s_stop[3];  // per entry segment (mod 3): the earliest stop request
-  __shared__ uint32_t s_next;     // wave 0's choice of the next entry
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t g = blockIdx.x, G = gridDim.x;
-  const uint32_t w = g * kLsWaves + wv;
-  const uint32_t n = tab->n, iters = tab->iters, poll_mask = tab->poll_mask, budget = tab->budget;
-  const uint64_t yield_base = tab->yield_base >> 32;
-  unsigned long long* const done_base = &st->done[0][(w % kPoolDoneShards) * 8];
-  if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
-  __syncthreads();
-
-  uint32_t e = g % n, seg = 0;
-  PoolCursor c;
-  pool_load_ls<LD>(&tab->e[e], c, g, wv, G, n, e, iters);
-  uint32_t it = 0;
-  bool end = false;
-  for (;;) {
-    uint32_t done = 0;
-    const uint32_t sw = seg % 3;
-    while (it < c.it_end) {
-      // an LDS load, consumed after the hash (a volatile or generic-pointer read here compiled to a
-      // flat load waited on before the hash)
-      const uint32_t verdict = __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      const uint64_t dead = load_dead(st, c.slot);
-      const bool poll = ((it + w) & poll_mask) == 0;
-      uint64_t kill, yld;
-      if (__builtin_expect(poll, 0)) {
-        kill = __hip_atomic_load(&mb->kill[c.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        yld = __hip_atomic_load(&mb->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >> 32;
-      }
-      const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
-      const uint32_t it0 = it;
-      const uint32_t b = it * c.K + c.j;
-      const uint64_t nonce = c.base + ((uint64_t)b << 6) + lane;
-      uint64_t value;
-      if constexpr (LD)
-        value = npow_asm_work_value_lockstep_ld(nonce, c.up);
-      else
-        value = npow_asm_work_value_lockstep(nonce, c.u);
-      ++it;
-      bool hit = value >= c.threshold;
-      if constexpr (BOUNDED) {
-        const uint32_t in_lanes = b < c.last_b ? 64u : (b == c.last_b ? c.tail : 0u);
-        hit = hit && lane < in_lanes;
-        done += in_lanes;
-      } else {
-        done += 64;
-      }
-      const uint64_t hits = __ballot(hit);
-      bool leave = hits != 0;  // wave-uniform (scalar): leave the entry
-      if (__builtin_expect(hits != 0, 0)) {
-        const int wl = __builtin_ctzll(hits);
-        const uint64_t wn = readlane64(nonce, wl), wval = readlane64(value, wl);
-        if (lane == 0) {
-          if (atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen) < c.gen) {  // first win
-            PoolWin* pw = &mb->win[c.slot];
-            __hip_atomic_store(&pw->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&pw->value, wval, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            __hip_atomic_store(&pw->gen, c.gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-          }
-        }
-      }
-      if (__builtin_expect(poll, 0)) {
-        if (readlane64(yld, 0) != yield_base) {  // new jobs wait: end every unbounded entry (pool_body)
-          if (lane == 0)
-            for (uint32_t k = 0; k < n; ++k)
-              if (!tab->e[k].bounded) atomicMax(&st->slot[tab->e[k].slot].dead, (unsigned long long)tab->e[k].gen);
-          leave = leave || !c.bounded;
-        }
-        if (readlane64(kill, 0) == c.gen) {
-          if (lane == 0) atomicMax(&st->slot[c.slot].dead, (unsigned long long)c.gen);  // relay
-          leave = true;
-        }
-      }
-      leave = leave || readlane64(dead, 0) == c.gen;
-      const bool late = budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget;  // end the launch
-      if (__builtin_expect(leave || late, 0)) {
-        if (lane == 0)
-          __hip_atomic_fetch_min(&s_stop[sw], (it << 1) | (late ? 0u : 1u), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_WORKGROUP);
-        lds_drain();  // complete before the next hash's first barrier
-      }
-      // the word as read before this hash: requests with value < it0 were filed at the end of
-      // iteration it0 - 2 or earlier, behind the previous hash's barriers, so every wave saw
-      // them (a later one, value it0, some waves may have seen: all ignore it) -- one verdict
-      const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(verdict);
-      if ((v >> 1) < it0) {
-        end = (v & 1) == 0;
-        break;
-      }
-    }
-    if (lane == 0 && done) atomicAdd(done_base + (size_t)c.slot * (kPoolDoneShards * 8), (unsigned long long)done);
-    if (it >= iters || end) break;
-    // leave the entry (its bounded range is used up, or a request): wave 0 picks the next live
-    // unbounded entry, cyclic from e + 1, and resets the request word of the next segment
-    if (wv == 0) {
-      uint32_t next = n;
-      for (uint32_t k = 1; k < n; ++k) {
-        uint32_t e2 = e + k;
-        if (e2 >= n) e2 -= n;
-        const PoolEntry* pe = &tab->e[e2];
-        if (pe->bounded) continue;
-        if (load_dead(st, pe->slot) >= pe->gen) continue;
-        next = e2;
-        break;
-      }
-      if (lane == 0) {
-        s_next = next;
-        s_stop[(seg + 1) % 3] = ~0u;
-      }
-    }
-    __syncthreads();
-    const uint32_t next =
-        __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-    if (next == n) break;
-    e = next;
-    ++seg;
-    pool_load_ls<LD>(&tab->e[e], c, g, wv, G, n, e, iters);
-  }
-}
-
 // Live in-kernel clock (PoolClk): the first wave of workgroups 0..kClkWaves-1 -- one per XCD,
 // workgroups are dealt to XCDs round-robin -- reads s_memtime after its first instruction and
 // both counters after its last; 2 scalar reads and one 24-byte store per 4,096 waves.
 __device__ __forceinline__ bool clk_wave() { return blockIdx.x < (unsigned)kClkWaves && threadIdx.x < 64; }
-__device__ __forceinline__ uint64_t clk_begin() { return clk_wave() ? __builtin_amdgcn_s_memtime() : 0; }
 // The two-group kernels keep the start in LDS: a register live across the whole kernel was spilled to
 // scratch by every wave (8 bytes per lane: ~4 MB written and read back per launch, in PMC).
 __shared__ uint64_t s_clk_start;
@@ -768,23 +340,24 @@ __device__ __forceinline__ void clk_end_ls2(const PoolTable* tab, PoolMailbox* m
     __hip_atomic_store(&r->seq, tab->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
-__device__ __forceinline__ void clk_end(const PoolTable* tab, PoolMailbox* mb, uint64_t t_start, uint64_t c_start) {
-  if (!clk_wave()) return;
-  const uint64_t c_end = __builtin_amdgcn_s_memtime();
-  const uint64_t t_end = __builtin_amdgcn_s_memrealtime();
-  if (threadIdx.x == 0) {
-    PoolClk* r = &mb->clk[tab->ring & 3][blockIdx.x];
-    __hip_atomic_store(&r->cycles, c_end - c_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&r->ref, t_end - t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&r->seq, tab->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-// The two-workgroups-per-CU form (npow_pool_kernel_ls2*): the same protocol as pool_body_ls with
-// the register budget of 8 waves per SIMD (64 VGPRs, 80 SGPRs, of which the stream takes 38 for
-// the uniforms it loads itself).  The loop keeps only what every iteration needs in registers:
-// the nonce advances in a VGPR by K * 64, the block index by K; the entry's fields, the table and
-// the mailbox are re-read inside the rare branches (a win, a poll, leaving an entry).
+// The search body (npow_pool_kernel_ls2*): two 1,024-lane workgroups per CU put 8 waves on every
+// SIMD, in two lockstep groups, and the stream's s_barrier after every interval keeps each group's
+// waves in the same phase.  Every wave of a workgroup must therefore hash the
+// same number of times, so everything that ends a wave's loop is decided per workgroup:
+//  * a workgroup works on one entry at a time (its own entry g % n first; bounded entries are dense
+//    over their own workgroups' waves, PoolEntry comment with unit = workgroup);
+//  * a wave that wants its workgroup to stop (a win, a dead / killed / yielded entry, the time
+//    budget) files a request in LDS, s_stop[segment % 3] = min((it + 1) << 1 | kind) with kind 0 =
+//    end the launch, 1 = leave the entry, drained before the iteration's closing s_barrier; every
+//    wave reads the word at the top of an iteration, so all waves see the same set of requests and
+//    leave together, one hash after the request (~16 us);
+//  * leaving an entry: wave 0 picks the next entry and broadcasts it through LDS (one
+//    __syncthreads); each entry segment has its own request word (3 rotate: the word of segment
+//    s + 1 is reset at the end of segment s, after its last reader).
+// The register budget at 8 waves per SIMD is 64 VGPRs and 80 SGPRs, of which the stream takes 38 for
+// the uniforms it loads itself.  The loop keeps only what every iteration needs in registers: the
+// nonce advances in a VGPR by K * 64, the block index by K; the entry's fields, the table and the
+// mailbox are re-read inside the rare branches (a win, a poll, leaving an entry).
 //
 // Early finish: a won or killed entry usually shares its launch with live ones, which keep the
 // launch running for the rest of its budget; the job's nonce count would only be read back after
@@ -1022,8 +595,9 @@ __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st
 template <bool BOUNDED>
 __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
                                               PoolMailbox* __restrict__ mb, const uint64_t t_start) {
-  __shared__ uint32_t s_stop[3];  // per entry segment (mod 3): the earliest stop request (pool_body_ls)
-  __shared__ uint32_t s_flag;     // lane 0 of a polling wave -> its wave: leave the entry
+  __shared__ uint32_t s_stop[3];         // per entry segment (mod 3): the earliest stop request
+  __shared__ uint32_t s_flag[kLsWaves];  // lane 0 of a polling wave -> its wave: leave the entry (one word
+                                         // per wave: with a poll interval below 16, several waves poll at once)
   __shared__ uint32_t s_next;
   __shared__ uint32_t s_done[kLsWaves];  // each wave's nonces on the entry it is leaving
   __shared__ uint32_t s_seen;            // dynamic entries this workgroup has acquired for (ls2_fresh)
@@ -1049,7 +623,6 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     if (lane == 0) s_next = first;
   }
   __syncthreads();
-  (void)s_flag;
 
   uint32_t e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
   uint32_t seg = 0, it = 0;
@@ -1058,7 +631,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     if (e == kNoEntry) break;
     const PoolEntry* pe = (const PoolEntry*)ls2_entry(tab, mb, e);
     PoolCursor c;
-    pool_load_ls<true>(pe, c, g, wv, G, n, e, iters);
+    pool_load_ls(pe, c, g, wv, G, n, e, iters);
     const uint32_t sw = seg % 3;
     const uint32_t poll_mask = tab->poll_mask, budget = tab->budget;
     unsigned long long* const dead_p = &st->slot[c.slot].dead;
@@ -1096,10 +669,10 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
         }
       }
       if (__builtin_expect(((it0 + w) & poll_mask) == 0, 0)) {
-        if (lane == 0) s_flag = ls2_poll(tab, st, mb, e, &s_seen) ? 1u : 0u;  // the wave's own LDS word use:
-        lds_drain();                                                 // no other wave touches s_flag
+        if (lane == 0) s_flag[wv] = ls2_poll(tab, st, mb, e, &s_seen) ? 1u : 0u;  // the wave's own word
+        lds_drain();
         leave = leave || __builtin_amdgcn_readfirstlane(
-                             __hip_atomic_load(&s_flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) != 0;
+                             __hip_atomic_load(&s_flag[wv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) != 0;
       }
       leave = leave || readlane64(dead, 0) == gen;
       const bool late = budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget;
@@ -1113,8 +686,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       b += c.K;
       // The verdict as read before this hash holds every request filed before it: each one was
       // drained before the s_barrier below, which every wave passes before its next read.  So
-      // all waves see the same set and leave together, one hash after the request (pool_body_ls
-      // waits two: it has no barrier of its own between a request and the next read).
+      // all waves see the same set and leave together, one hash after the request.
       const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(verdict);
       if (v != ~0u) {
         end = (v & 1) == 0;
@@ -1147,64 +719,20 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   clk_end_ls2(tab, mb, t_start, wv);
 }
 
-
-// The table in device memory (uploaded in stream order before the launch).
-template <bool BOUNDED>
-__global__ __launch_bounds__(kBlock)
-#if NPOW_POOL_NUM_SGPR
-__attribute__((amdgpu_num_sgpr(NPOW_POOL_NUM_SGPR)))
+// NPOW_LS2_PRIO (A/B builds, tools/experiments/setprio_ab.py; 0 = off): a static s_setprio 1 before
+// the loop for one half of the waves -- 1: the second-dispatched workgroup of each CU (blockIdx.x >=
+// gridDim.x / 2), 2: waves 8..15 of every workgroup, 3: waves 0..7 (control for 2).
+#ifndef NPOW_LS2_PRIO
+#define NPOW_LS2_PRIO 0
 #endif
-void npow_pool_kernel(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
-                      PoolMailbox* __restrict__ mb) {
-  uint64_t t_start;  // first instruction: see pool_body
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
-  const uint64_t c_start = clk_begin();
-  pool_body<BOUNDED>(tab, st, mb, t_start);
-  clk_end(tab, mb, t_start, c_start);
-}
-
-// Up to kArgEntries entries: the table travels in the launch's kernel arguments, so no copy
-// has to run on the stream before the kernel (a blit dispatch, several microseconds of every
-// search's latency).  The body reads it in place through the kernarg segment pointer (taking
-// the address of a by-value parameter would copy it to scratch).
-template <bool BOUNDED>
-__global__ __launch_bounds__(kBlock)
-#if NPOW_POOL_NUM_SGPR
-__attribute__((amdgpu_num_sgpr(NPOW_POOL_NUM_SGPR)))
+__device__ __forceinline__ void ls2_static_prio() {
+#if NPOW_LS2_PRIO == 1
+  if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
+#elif NPOW_LS2_PRIO == 2
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= kLsWaves / 2) __builtin_amdgcn_s_setprio(1);
+#elif NPOW_LS2_PRIO == 3
+  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < kLsWaves / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-void npow_pool_kernel_arg(const PoolTableArg targ, PoolDevState* __restrict__ st, PoolMailbox* __restrict__ mb) {
-  uint64_t t_start;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
-  (void)targ;
-  const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();  // address space 4 -> generic
-  const uint64_t c_start = clk_begin();
-  pool_body<BOUNDED>(tab, st, mb, t_start);
-  clk_end(tab, mb, t_start, c_start);
-}
-
-// The lockstep variants: 1,024-lane workgroups, one per CU (pool_body_ls); ls2: two per CU.
-template <bool BOUNDED>
-__global__ __launch_bounds__(kLsBlock) void npow_pool_kernel_ls(const PoolTable* __restrict__ tab,
-                                                               PoolDevState* __restrict__ st,
-                                                               PoolMailbox* __restrict__ mb) {
-  uint64_t t_start;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
-  const uint64_t c_start = clk_begin();
-  pool_body_ls<BOUNDED, false>(tab, st, mb, t_start);
-  clk_end(tab, mb, t_start, c_start);
-}
-
-template <bool BOUNDED>
-__global__ __launch_bounds__(kLsBlock) void npow_pool_kernel_ls_arg(const PoolTableArg targ,
-                                                                   PoolDevState* __restrict__ st,
-                                                                   PoolMailbox* __restrict__ mb) {
-  uint64_t t_start;
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
-  (void)targ;
-  const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();
-  const uint64_t c_start = clk_begin();
-  pool_body_ls<BOUNDED, false>(tab, st, mb, t_start);
-  clk_end(tab, mb, t_start, c_start);
 }
 
 template <bool BOUNDED>
@@ -1214,6 +742,7 @@ __global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2(const PoolTa
   uint64_t t_start;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
   clk_begin_lds();
+  ls2_static_prio();
   pool_body_ls2<BOUNDED>(tab, st, mb, t_start);  // records the clock at its end (clk_end_ls2)
 }
 
@@ -1226,49 +755,28 @@ __global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2_arg(const Po
   (void)targ;
   const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();
   clk_begin_lds();
+  ls2_static_prio();
   pool_body_ls2<BOUNDED>(tab, st, mb, t_start);  // records the clock at its end (clk_end_ls2)
 }
 
-hipError_t launch_pool(const PoolShape& sh, hipStream_t stream, const PoolTable* tab, bool bounded, PoolDevState* st,
+hipError_t launch_pool(hipStream_t stream, int grid, const PoolTable* tab, bool bounded, PoolDevState* st,
                        PoolMailbox* mb) {
-  if (sh.lockstep && sh.groups == 2) {
-    if (bounded)
-      npow_pool_kernel_ls2<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
-    else
-      npow_pool_kernel_ls2<false><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
-  } else if (sh.lockstep) {
-    if (bounded)
-      npow_pool_kernel_ls<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
-    else
-      npow_pool_kernel_ls<false><<<sh.grid, kLsBlock, sh.lds, stream>>>(tab, st, mb);
-  } else if (bounded) {
-    npow_pool_kernel<true><<<sh.grid, kBlock, 0, stream>>>(tab, st, mb);
-  } else {
-    npow_pool_kernel<false><<<sh.grid, kBlock, 0, stream>>>(tab, st, mb);
-  }
+  if (bounded)
+    npow_pool_kernel_ls2<true><<<grid, kLsBlock, 0, stream>>>(tab, st, mb);
+  else
+    npow_pool_kernel_ls2<false><<<grid, kLsBlock, 0, stream>>>(tab, st, mb);
   return hipGetLastError();
 }
 
-hipError_t launch_pool_arg(const PoolShape& sh, hipStream_t stream, const PoolTable& host_tab, bool bounded,
-                           PoolDevState* st, PoolMailbox* mb) {
+hipError_t launch_pool_arg(hipStream_t stream, int grid, const PoolTable& host_tab, bool bounded, PoolDevState* st,
+                           PoolMailbox* mb) {
   if (host_tab.n > (uint32_t)kArgEntries) return hipErrorInvalidValue;
   PoolTableArg a;
   memcpy(&a, &host_tab, pool_table_bytes(host_tab.n));
-  if (sh.lockstep && sh.groups == 2) {
-    if (bounded)
-      npow_pool_kernel_ls2_arg<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
-    else
-      npow_pool_kernel_ls2_arg<false><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
-  } else if (sh.lockstep) {
-    if (bounded)
-      npow_pool_kernel_ls_arg<true><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
-    else
-      npow_pool_kernel_ls_arg<false><<<sh.grid, kLsBlock, sh.lds, stream>>>(a, st, mb);
-  } else if (bounded) {
-    npow_pool_kernel_arg<true><<<sh.grid, kBlock, 0, stream>>>(a, st, mb);
-  } else {
-    npow_pool_kernel_arg<false><<<sh.grid, kBlock, 0, stream>>>(a, st, mb);
-  }
+  if (bounded)
+    npow_pool_kernel_ls2_arg<true><<<grid, kLsBlock, 0, stream>>>(a, st, mb);
+  else
+    npow_pool_kernel_ls2_arg<false><<<grid, kLsBlock, 0, stream>>>(a, st, mb);
   return hipGetLastError();
 }
 
@@ -1287,16 +795,13 @@ hipError_t launch_task(Mode mode, int grid, hipStream_t stream, const LaunchArgs
                        HostMailbox* mb, uint64_t* out) {
   switch (mode) {
     case Mode::kSweep:
-      npow_task_kernel<Mode::kSweep><<<grid, kBlock, 0, stream>>>(a, st, mb, out);
-      break;
-    case Mode::kSweepLs:
-      npow_sweep_kernel_ls<<<grid, kLsBlock, 0, stream>>>(a, st, mb, out);
-      break;
-    case Mode::kSweepLs2:
       npow_sweep_kernel_ls2<<<grid, kLsBlock, 0, stream>>>(a, st, mb, out);
       break;
     case Mode::kValues:
-      npow_task_kernel<Mode::kValues><<<grid, kBlock, 0, stream>>>(a, st, mb, out);
+      npow_values_kernel_ls2<<<grid, kLsBlock, 0, stream>>>(a, st, out);
+      break;
+    case Mode::kValuesSeq:
+      npow_values_kernel_seq<<<grid, kBlock, 0, stream>>>(a, st, out);
       break;
   }
   return hipGetLastError();

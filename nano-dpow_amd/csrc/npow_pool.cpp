@@ -1,6 +1,6 @@
 // npow_pool.cpp -- the work pool of libnanopow.so: every first-win search (npow_search,
 // npow_search_batch, npow_submit) is a job; up to max_active jobs are searched at once,
-// all of them by ONE kernel launch per device (npow_pool_kernel), each on a disjoint
+// all of them by ONE kernel launch per device (npow_pool_kernel_ls2*), each on a disjoint
 // per-device stride of its nonce space.
 //
 // Replaces the request queue and GPU loop of the reference work server
@@ -12,9 +12,9 @@
 // The reference serves ONE root at a time; a DPoW burst (many work_generate requests in
 // flight, client/work_handler.py:83-125 per client) is served here by keeping up to
 // kMaxSlots roots live in every launch, so a root that is won mid-launch costs nothing:
-// its waves move on to the other live roots (npow_kernel.hip, npow_pool_kernel).
+// its workgroups move on to the other live roots (npow_kernel.hip, pool_body_ls2).
 //
-// With the two-group kernel (the default) a job also leaves its launch early in both directions:
+// A job also leaves its launch early in both directions:
 // a won or killed job finishes from the final nonce count the kernel publishes once no workgroup is
 // left on its entry (early_finish; PoolMailbox::fin), and a new unbounded job joins the running
 // launch as a dynamic entry (dyn_add; PoolMailbox::dyn) instead of ending it (yield_if_long, now
@@ -33,9 +33,11 @@
 // skips it from then on, and every job it held hands the part of its nonce range the device
 // had not finished to the job's surviving devices (re-striding; a bounded job's range stays
 // covered exactly once more).  A job fails only when no device is left to search it.
-// Test hooks (environment, read once): NANOPOW_FAULT_INVALID=d[,d...] makes the host read a
-// corrupted value for every win of those logical devices; NANOPOW_FAULT_HIP=d:n makes device
-// d's launches fail after its n-th.  (npow_engine.cpp: NANOPOW_FAULT_INIT=d fails npow_init on d.)
+// Test hooks (environment, read once, and only with NANOPOW_TEST_HOOKS=1 beside them -- a stray
+// variable in a deployment must not drop GPUs; an active hook is reported on stderr):
+// NANOPOW_FAULT_INVALID=d[,d...] makes the host read a corrupted value for every win of those
+// logical devices; NANOPOW_FAULT_HIP=d:n makes device d's launches fail after its n-th.
+// (npow_engine.cpp: NANOPOW_FAULT_INIT=d fails npow_init on d.)
 #include <hip/hip_runtime.h>
 #include <sys/prctl.h>
 #include <time.h>
@@ -72,6 +74,7 @@ constexpr double kPrelaunchUs = 2000.0;  // queue the next launch when the runni
 constexpr double kDynMinUs = 3000.0;     // join a running launch only with this much budget left
 constexpr double kFreshSpinUs = 400.0;   // poll without sleeping this long after a launch starts (quick wins)
 constexpr int kInvalidStreakMax = 3;     // consecutive invalid results that drop a device (@1669144)
+constexpr double kStopSpinUs = 2000.0;   // nap(): poll without sleeping this long after a slot's job stopped
 // Between steps a worker with a launch in flight sleeps this long (wakes early on new jobs):
 // a win is seen within it, and the thread costs ~6 % of a core instead of spinning (nap()).
 // NANOPOW_POLL_US overrides (0 = spin).
@@ -90,9 +93,23 @@ struct Faults {
   int hip_dev = -1;           // logical device whose launches fail ...
   uint64_t hip_after = 0;     // ... after this many
 };
+}  // namespace
+bool test_hooks_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("NANOPOW_TEST_HOOKS");
+    return e && strcmp(e, "1") == 0;
+  }();
+  return on;
+}
+namespace {
 const Faults& faults() {
   static const Faults f = [] {
     Faults x;
+    if (!test_hooks_enabled()) {
+      if (getenv("NANOPOW_FAULT_INVALID") || getenv("NANOPOW_FAULT_HIP"))
+        fprintf(stderr, "nanopow: NANOPOW_FAULT_* ignored (test hooks need NANOPOW_TEST_HOOKS=1)\n");
+      return x;
+    }
     if (const char* e = getenv("NANOPOW_FAULT_INVALID")) {
       for (const char* p = e; *p;) {
         char* end = nullptr;
@@ -107,6 +124,9 @@ const Faults& faults() {
       x.hip_dev = (int)strtol(e, &end, 10);
       if (end && *end == ':') x.hip_after = strtoull(end + 1, nullptr, 10);
     }
+    if (x.invalid_mask || x.hip_dev >= 0)
+      fprintf(stderr, "nanopow: TEST HOOKS ACTIVE: corrupt wins of device mask %#llx, fail launches of device %d after %llu\n",
+              (unsigned long long)x.invalid_mask, x.hip_dev, (unsigned long long)x.hip_after);
     return x;
   }();
   return f;
@@ -135,6 +155,10 @@ struct Job {
   std::vector<uint8_t> on_dev;      // per device k: a slot holds the job
   std::vector<uint8_t> seen_dev;    // per device k: adopted at least once (re-adoptions do not yield)
   std::vector<uint8_t> dev_done;    // per device k: finished with the job
+  std::vector<int> dev_slot;        // per device k: the slot holding it while on_dev[k] ...
+  std::vector<uint64_t> dev_gen;    // ... and its generation there (the decider raises their kill words)
+  std::vector<double> t_stop;       // per device k: when its worker saw it stop hashing the job (us; 0 = never adopted)
+  int winner_k = -1;                // the device whose result decided the job
   int pending_devs = 0;
   bool admitted = false;
   bool lost = false;                // a dead device's remainder had no surviving device to go to
@@ -150,8 +174,9 @@ struct Job {
   std::atomic<bool> cancel_req{false};
 
   bool cancel_seen() const { return cancel_req.load(std::memory_order_relaxed) || (cancel && load_acquire(cancel)); }
-  // NANOPOW_TRACE_LATENCY: host timestamps of the job's life (steady clock, us), printed by pool_wait
-  double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0;
+  // host timestamps of the job's life (steady clock, us): t_submit, t_decide and t_finish always
+  // (npow_wait_info), the rest for NANOPOW_TRACE_LATENCY, which prints them in pool_wait
+  double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0, t_decide = 0;
 };
 using JobP = std::shared_ptr<Job>;
 
@@ -165,6 +190,7 @@ struct Pool {
   uint32_t max_active = kMaxSlots;
   bool running = false;
   std::atomic<uint64_t> version{0};  // bumped whenever `active` gains a job
+  std::atomic<uint64_t> decisions{0};  // bumped when a job split over devices is decided: wakes napping workers
 } g_pool;
 
 std::atomic<uint64_t> g_gen{0};
@@ -202,7 +228,7 @@ void finish_locked(const JobP& j) {
     else j->status = NPOW_EXHAUSTED;
     j->decided = true;
   }
-  if (g_trace_lat) j->t_finish = now_us();
+  j->t_finish = now_us();
   j->finished = true;
   auto it = std::find(g_pool.active.begin(), g_pool.active.end(), j);
   if (it != g_pool.active.end()) g_pool.active.erase(it);
@@ -217,6 +243,7 @@ void device_done_locked(const JobP& j, size_t k) {
   if (j->dev_done[k]) return;
   j->dev_done[k] = 1;
   j->on_dev[k] = 0;
+  if (j->seen_dev[k] && j->t_stop[k] == 0) j->t_stop[k] = now_us();
   if (--j->pending_devs == 0) finish_locked(j);
 }
 
@@ -257,6 +284,25 @@ void abandon_locked(const JobP& j, size_t k, int code, const std::string& msg) {
   device_done_locked(j, k);
 }
 
+// Job j has just been decided by device k_win's result: raise the kill word of every other device
+// that holds it now, instead of waiting for that device's worker to notice the decision at its next
+// step (it naps up to g_poll_us between steps), and wake the napping workers.  Each slot's kill
+// word is the job's generation there; a slot reused later has a larger generation, so a late store
+// could not stop another job -- and cannot happen anyway: a device releases a slot only under
+// g_pool.mu, after device_done_locked or a re-arm cleared on_dev.
+void stop_other_devices_locked(Job& j, size_t k_win) {
+  if (j.devs.size() < 2) return;
+  for (size_t k = 0; k < j.devs.size(); ++k) {
+    if (k == k_win || !j.on_dev[k] || j.dev_slot[k] < 0) continue;
+    Device& d = *g_devs[(size_t)j.devs[k]];
+    __atomic_store_n(&d.pmb->kill[j.dev_slot[k]], j.dev_gen[k], __ATOMIC_RELEASE);
+    std::lock_guard<std::mutex> sg(d.stats_mu);
+    d.kills_relayed++;
+  }
+  g_pool.decisions.fetch_add(1, std::memory_order_release);
+  g_pool.cv_work.notify_all();
+}
+
 // -- one device's worker ------------------------------------------------------------------------
 enum class SlotState { kFree, kActive, kDraining };
 
@@ -274,6 +320,8 @@ struct Slot {
   bool new_job = false;    // adopted for the first time on this device (not a re-adoption)
   bool fin_seen = false;   // the kernel published this generation's final count (PoolMailbox::fin) ...
   bool early = false;      // ... and the job was finished from it before retiring
+  double stop_us = 0;      // the job was won or killed at this time: the worker polls without napping
+                           // until the slot's final count is in (a quick return, and an exact stop time)
   struct Issued {
     uint64_t seq, base, count;
   };
@@ -329,7 +377,8 @@ class Worker {
   int queue_readbacks();
   int retire();
   void fail_all(const std::string& msg);
-  void push_back_locked(Slot& sl, size_t from);
+  void push_back_locked(Slot& sl, size_t from, bool skip_done = false);
+  bool launch_completed(uint64_t seq) const;
   void account_clock(int ring, uint64_t seq);
   int step();
   void nap();
@@ -376,9 +425,12 @@ void Worker::adopt() {
     sl.k = (size_t)k;
     sl.gen = ++g_gen;
     sl.win_seen = sl.requeue = sl.no_more = sl.readback = sl.fin_seen = sl.early = false;
+    sl.stop_us = 0;
     sl.fresh = true;
     sl.inflight.clear();
     j->on_dev[k] = 1;
+    j->dev_slot[k] = s;
+    j->dev_gen[k] = sl.gen;
     if (g_trace_lat && j->t_adopt == 0) j->t_adopt = now_us();
     sl.new_job = !j->seen_dev[k];
     if (sl.new_job) adopted = true;  // a new job: worth ending a long launch for
@@ -405,7 +457,6 @@ bool Worker::dyn_add(int s) {
   Job& j = *sl.job;
   if (q_.size() != 1 || j.max_per_dev || g_budget_us.load() == 0) return false;
   const PoolShape sh = pool_shape(d_);
-  if (!sh.lockstep || sh.groups != 2) return false;
   const PoolInflight& f = q_.front();
   if (!f.counted) return false;  // a one-entry launch: the new job ends it (a yield) instead
   if ((uint32_t)((uint32_t)ctl_ - (uint32_t)f.dyn_base) >= (uint32_t)kDynEntries) return false;
@@ -494,7 +545,12 @@ void Worker::handle_win(int s) {
   if (g_trace_lat && j.t_win == 0) j.t_win = now_us();
   if (cpu_v == v && v >= j.threshold) {
     invalid_streak_ = 0;
-    decide_locked(j, NPOW_OK, n, v);
+    if (j.status == kPending) {
+      decide_locked(j, NPOW_OK, n, v);
+      j.t_decide = now_us();
+      j.winner_k = (int)sl.k;
+      stop_other_devices_locked(j, sl.k);
+    }
   } else {
     // "GPU returned invalid work": the launches that held this generation stopped at the win,
     // so a bounded job gets back every range from the one holding the winner on; the job is
@@ -524,15 +580,34 @@ void Worker::handle_win(int s) {
     }
   }
   sl.state = SlotState::kDraining;  // the winning wave already marked the slot dead on the device
+  sl.stop_us = now_us();
 }
 
 // Ranges sl.inflight[from..] did not complete (their launches stopped on this generation or
-// failed): hand them back to the front of the job's queue for this device, in order.
-void Worker::push_back_locked(Slot& sl, size_t from) {
+// failed): hand them back to the front of the job's queue for this device, in order.  With
+// skip_done, a range whose launch has already completed on the GPU (retire() has not seen it yet)
+// stays: it was hashed in full, and handing it back would hash it again and over-count the job's
+// nonces_done (a dropped device's check_slots / fail_all).
+void Worker::push_back_locked(Slot& sl, size_t from, bool skip_done) {
   Job& j = *sl.job;
-  for (size_t i = sl.inflight.size(); i > from; --i)
-    j.todo[sl.k].push_front({sl.inflight[i - 1].base, sl.inflight[i - 1].count});
-  sl.inflight.resize(from);
+  std::vector<Slot::Issued> keep(sl.inflight.begin(), sl.inflight.begin() + (ptrdiff_t)from);
+  for (size_t i = sl.inflight.size(); i > from; --i) {
+    const Slot::Issued& r = sl.inflight[i - 1];
+    if (skip_done && launch_completed(r.seq)) {
+      keep.insert(keep.begin() + (ptrdiff_t)from, r);
+      continue;
+    }
+    j.todo[sl.k].push_front({r.base, r.count});
+  }
+  sl.inflight.swap(keep);
+}
+
+// The launch with sequence number seq has completed on the GPU (its stop event has fired, or
+// retire() already dropped it).
+bool Worker::launch_completed(uint64_t seq) const {
+  for (const PoolInflight& f : q_)
+    if (f.seq == seq) return hipEventQuery(d_.ev_stop[f.ring]) == hipSuccess;
+  return true;
 }
 
 // The launch's in-kernel clock records (PoolClk, one per XCD) into the device statistics.
@@ -592,7 +667,7 @@ void Worker::check_slots() {
     if (d_.dead) {  // dropped device: stop every job's waves; retire() re-strides them
       if (j.max_per_dev) {  // the killed launches leave their ranges unfinished: hand them back
         std::lock_guard<std::mutex> g(g_pool.mu);
-        push_back_locked(sl, 0);
+        push_back_locked(sl, 0, true);
       }
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);
       sl.state = SlotState::kDraining;
@@ -604,6 +679,7 @@ void Worker::check_slots() {
       }
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);  // in-flight waves stop
       sl.state = SlotState::kDraining;
+      sl.stop_us = now_us();
     } else if (sl.no_more) {
       sl.state = SlotState::kDraining;
     }
@@ -691,19 +767,20 @@ int Worker::launch() {
   const int r = ring_;
   ring_ = (ring_ + 1) % kEventRing;
   const size_t bytes = pool_table_bytes(n);
-  // The table goes up in stream order right before its launch.  (Uploading it on a second
-  // stream beside the running launch, joined by an event, cost 1.5-2 % of kernel throughput:
-  // the copy is a blit kernel that competes with the running launch.)
-  static const bool force_upload = getenv("NANOPOW_TABLE_UPLOAD") != nullptr;  // A/B switch
+  // Up to kArgEntries entries the table rides in the kernel arguments (no copy before the launch;
+  // uploading it instead cost 2.5 %, profiles/r02_ab_table_upload.jsonl); a larger one goes up in
+  // stream order right before its launch.  (Uploading it on a second stream beside the running
+  // launch, joined by an event, cost 1.5-2 % of kernel throughput: the copy is a blit kernel that
+  // competes with the running launch.)
   if (faults().hip_dev == d_.id && seq_ > faults().hip_after)  // NANOPOW_FAULT_HIP (tests)
     return fail(NPOW_ERR_HIP, "injected launch failure (NANOPOW_FAULT_HIP)");
-  if (n <= (uint32_t)kArgEntries && !force_upload) {  // the table rides in the kernel arguments
+  if (n <= (uint32_t)kArgEntries) {
     HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
-    HIPTRY(launch_pool_arg(sh, d_.stream, t, bounded, d_.pst, d_.pmb_dev));
+    HIPTRY(launch_pool_arg(d_.stream, sh.grid, t, bounded, d_.pst, d_.pmb_dev));
   } else {
     HIPTRY(hipMemcpyAsync(d_.d_tab[r], d_.h_tab[r], bytes, hipMemcpyHostToDevice, d_.stream));
     HIPTRY(hipEventRecord(d_.ev_start[r], d_.stream));
-    HIPTRY(launch_pool(sh, d_.stream, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
+    HIPTRY(launch_pool(d_.stream, sh.grid, d_.d_tab[r], bounded, d_.pst, d_.pmb_dev));
   }
   HIPTRY(hipEventRecord(d_.ev_stop[r], d_.stream));
   if (q_.empty()) front_start_ = std::chrono::steady_clock::now();
@@ -812,7 +889,7 @@ void Worker::fail_all(const std::string& msg) {
   }
   for (Slot& sl : slots_) {
     if (sl.state == SlotState::kFree) continue;
-    if (sl.job->max_per_dev) push_back_locked(sl, 0);
+    if (sl.job->max_per_dev) push_back_locked(sl, 0, true);
     abandon_locked(sl.job, sl.k, d_.dead_code, d_.dead_msg);
     sl.job.reset();
     sl.inflight.clear();
@@ -907,6 +984,14 @@ void Worker::nap() {
     cpu_relax();
     return;
   }
+  // a won / killed slot drains within a hash or two (~20-40 us): poll until its count is in, for at
+  // most kStopSpinUs after the stop
+  const double t = now_us();
+  for (const Slot& sl : slots_)
+    if (sl.state == SlotState::kDraining && sl.stop_us > 0 && !sl.fin_seen && t - sl.stop_us < kStopSpinUs) {
+      cpu_relax();
+      return;
+    }
   const double since = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - front_start_).count();
   if (since < kFreshSpinUs) {
     cpu_relax();
@@ -923,9 +1008,11 @@ void Worker::nap() {
     us = std::min(us, until_prelaunch);
   }
   const uint64_t v = seen_version_;
+  const uint64_t dec = g_pool.decisions.load(std::memory_order_acquire);
   std::unique_lock<std::mutex> lk(g_pool.mu);
   g_pool.cv_work.wait_for(lk, std::chrono::duration<double, std::micro>(us), [&] {
-    return g_pool.version.load(std::memory_order_relaxed) != v || !g_pool.running || d_.tasks_waiting.load() > 0;
+    return g_pool.version.load(std::memory_order_relaxed) != v || !g_pool.running || d_.tasks_waiting.load() > 0 ||
+           g_pool.decisions.load(std::memory_order_relaxed) != dec;
   });
 }
 
@@ -1035,8 +1122,11 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   j->on_dev.assign(G, 0);
   j->seen_dev.assign(G, 0);
   j->dev_done.assign(G, 0);
+  j->dev_slot.assign(G, -1);
+  j->dev_gen.assign(G, 0);
+  j->t_stop.assign(G, 0.0);
   j->pending_devs = (int)G;
-  if (g_trace_lat) j->t_submit = now_us();
+  j->t_submit = now_us();
   std::lock_guard<std::mutex> g(g_pool.mu);
   if (!g_pool.running) return fail(NPOW_ERR_NOT_INITIALISED, "engine is shut down");
   j->ticket = g_pool.next_ticket++;
@@ -1047,7 +1137,8 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   return NPOW_OK;
 }
 
-int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done) {
+int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done,
+              npow_search_info* info) {
   std::unique_lock<std::mutex> lk(g_pool.mu);
   auto it = g_pool.tickets.find(ticket);
   if (it == g_pool.tickets.end()) return fail(NPOW_ERR_BAD_ARGUMENT, "unknown ticket");
@@ -1073,6 +1164,24 @@ int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* va
     }
   }
   if (nonces_done) *nonces_done = j->done;
+  if (info) {
+    info->winner_device = j->winner_k >= 0 ? j->devs[(size_t)j->winner_k] : -1;
+    info->n_devices = (int32_t)j->devs.size();
+    info->decide_us = j->t_decide > 0 ? j->t_decide - j->t_submit : 0.0;
+    info->finish_us = j->t_finish - j->t_submit;
+    double worst = 0.0, over = 0.0;
+    if (j->t_decide > 0)
+      for (size_t k = 0; k < j->devs.size(); ++k) {
+        if ((int)k == j->winner_k || j->t_stop[k] <= j->t_decide) continue;
+        const double span = j->t_stop[k] - j->t_decide;
+        worst = std::max(worst, span);
+        Device& d = *g_devs[(size_t)j->devs[k]];
+        std::lock_guard<std::mutex> sg(d.stats_mu);
+        if (d.kernel_ms > 0) over += span * 1e-3 * (double)d.nonces / d.kernel_ms;  // us x nonces per ms
+      }
+    info->stop_after_decide_us = worst;
+    info->overshoot_nonces = (uint64_t)over;
+  }
   if (g_trace_lat)
     fprintf(stderr, "nanopow-lat adopt %.1f launch %.1f win %.1f kend %.1f finish %.1f return %.1f\n",
             j->t_adopt - j->t_submit, j->t_launch - j->t_submit, j->t_win - j->t_submit, j->t_kend - j->t_submit,

@@ -30,6 +30,12 @@ NPOW_ERR_INVALID_WORK = -5
 NPOW_ERR_CAPACITY = -6
 NPOW_ERR_INTERNAL = -7
 
+NPOW_ABI_VERSION = 3
+# hash paths of npow_values_path
+NPOW_PATH_SEARCH = 0   # the stream the search and sweep kernels execute (two lockstep workgroups per CU)
+NPOW_PATH_SEQ = 1      # a second generated stream, scheduled without barriers
+NPOW_PATH_GENERIC = 2  # plain HIP C++ of the 12 rounds, one (root, nonce) per lane
+
 M64 = (1 << 64) - 1
 
 # Every symbol include/nanopow.h declares (tests/test_abi.py checks the export table).
@@ -38,7 +44,8 @@ EXPORTED_SYMBOLS = (
     "npow_search_batch", "npow_sweep", "npow_values", "npow_values_pairs", "npow_set_tuning",
     "npow_device_stats_get", "npow_device_stats_reset", "npow_version",
     "npow_submit", "npow_wait", "npow_cancel", "npow_pool_config", "npow_pool_status",
-    "npow_set_pool_tuning",
+    "npow_set_pool_tuning", "npow_values_path", "npow_wait_info", "npow_device_stats_get_sized",
+    "npow_abi_version",
 )
 
 
@@ -66,6 +73,24 @@ class DeviceStats(ctypes.Structure):
         ("early_mismatches", ctypes.c_uint64),
         ("yields", ctypes.c_uint64),
         ("dyn_entries", ctypes.c_uint64),
+        ("kills_relayed", ctypes.c_uint64),  # ABI 3
+    ]
+
+
+class SearchInfo(ctypes.Structure):
+    """npow_search_info: one search's outcome and host timeline (us since npow_submit)."""
+    _fields_ = [
+        ("size", ctypes.c_uint32),
+        ("status", ctypes.c_int32),
+        ("nonce", ctypes.c_uint64),
+        ("value", ctypes.c_uint64),
+        ("nonces_done", ctypes.c_uint64),
+        ("winner_device", ctypes.c_int32),
+        ("n_devices", ctypes.c_int32),
+        ("decide_us", ctypes.c_double),
+        ("finish_us", ctypes.c_double),
+        ("stop_after_decide_us", ctypes.c_double),
+        ("overshoot_nonces", ctypes.c_uint64),
     ]
 
 
@@ -141,6 +166,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.npow_pool_status.restype = ctypes.c_int
         lib.npow_set_pool_tuning.argtypes = [u32, u32]
         lib.npow_set_pool_tuning.restype = ctypes.c_int
+        lib.npow_values_path.argtypes = [ctypes.c_int, u8p, u64, u64, ctypes.c_int, p]
+        lib.npow_values_path.restype = ctypes.c_int
+        lib.npow_wait_info.argtypes = [u64, ctypes.c_int64, ctypes.POINTER(SearchInfo)]
+        lib.npow_wait_info.restype = ctypes.c_int
+        lib.npow_device_stats_get_sized.argtypes = [ctypes.c_int, ctypes.POINTER(DeviceStats), u64]
+        lib.npow_device_stats_get_sized.restype = ctypes.c_int
+        lib.npow_abi_version.argtypes = []
+        lib.npow_abi_version.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -207,6 +240,25 @@ class Ticket:
         self.result = (SearchResult(rc, nonce.value, value.value, done.value) if rc == NPOW_OK
                        else SearchResult(rc, None, None, done.value))
         return self.result
+
+    def wait_info(self, timeout: Optional[float] = None) -> Optional[SearchInfo]:
+        """wait() with the search's timeline (npow_wait_info): winner device, host times of the
+        decision and the finish, and the other devices' overshoot after the decision.  None if
+        still running after `timeout` seconds."""
+        if self.result is not None:
+            raise RuntimeError("the ticket's result was already collected")
+        lib = self.engine.lib
+        info = SearchInfo()
+        info.size = ctypes.sizeof(SearchInfo)
+        us = -1 if timeout is None else max(0, int(timeout * 1e6))
+        rc = lib.npow_wait_info(self.ticket, us, ctypes.byref(info))
+        if rc == NPOW_PENDING:
+            return None
+        self.cancel_token = None
+        _check(rc, lib, ok=(NPOW_OK, NPOW_CANCELLED, NPOW_EXHAUSTED))
+        self.result = (SearchResult(rc, info.nonce, info.value, info.nonces_done) if rc == NPOW_OK
+                       else SearchResult(rc, None, None, info.nonces_done))
+        return info
 
     def cancel(self) -> None:
         if self.result is None:
@@ -321,10 +373,23 @@ class Engine:
             raise NanoPowError(r.status, f"sweep cancelled after {r.total} hits: the hit set is partial")
         return r.hits
 
-    def values(self, root: bytes, start: int, count: int, device: int = 0) -> List[int]:
+    def values(self, root: bytes, start: int, count: int, device: int = 0, path: Optional[int] = None) -> List[int]:
+        """Work values of start .. start + count - 1: npow_values (the search kernels' stream), or
+        npow_values_path with an NPOW_PATH_* constant."""
         out = (ctypes.c_uint64 * max(count, 1))()
-        _check(self.lib.npow_values(device, _root(root), start & M64, count, ctypes.addressof(out)), self.lib)
+        if path is None:
+            rc = self.lib.npow_values(device, _root(root), start & M64, count, ctypes.addressof(out))
+        else:
+            rc = self.lib.npow_values_path(device, _root(root), start & M64, count, path, ctypes.addressof(out))
+        _check(rc, self.lib)
         return list(out[:count])
+
+    def values_array(self, root: bytes, start: int, count: int, device: int = 0, path: int = NPOW_PATH_SEARCH):
+        """The same as values() into a numpy uint64 array (large ranges)."""
+        import numpy as np
+        out = np.empty(max(count, 1), dtype=np.uint64)
+        _check(self.lib.npow_values_path(device, _root(root), start & M64, count, path, out.ctypes.data), self.lib)
+        return out[:count]
 
     def values_pairs(self, roots: Sequence[bytes], nonces: Sequence[int], device: int = 0) -> List[int]:
         n = len(nonces)
@@ -349,12 +414,11 @@ class Engine:
 
     def stats(self, device: int = 0) -> DeviceStats:
         s = DeviceStats()
-        _check(self.lib.npow_device_stats_get(device, ctypes.byref(s)), self.lib)
+        _check(self.lib.npow_device_stats_get_sized(device, ctypes.byref(s), ctypes.sizeof(s)), self.lib)
         return s
 
-    def pool_kernel_groups(self, device: int = 0) -> int:
-        """The search kernel in use: 0 = seq, 1 / 2 = lockstep workgroups per CU (2: early finish)."""
-        return int(self.stats(device).pool_groups)
+    def abi_version(self) -> int:
+        return int(self.lib.npow_abi_version())
 
     def reset_stats(self, device: int = 0) -> None:
         _check(self.lib.npow_device_stats_reset(device), self.lib)

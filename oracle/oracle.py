@@ -51,6 +51,8 @@ def _load() -> ctypes.CDLL:
         lib.oracle_blake2b.argtypes = [p, ctypes.c_size_t, ctypes.c_char_p, ctypes.c_size_t]
         lib.oracle_sweep.restype = u64
         lib.oracle_sweep.argtypes = [ctypes.c_char_p, u64, u64, u64, p, u64, ctypes.c_int]
+        lib.oracle_values_range.restype = ctypes.c_int
+        lib.oracle_values_range.argtypes = [ctypes.c_char_p, u64, u64, p, ctypes.c_int]
         lib.oracle_search.restype = u64
         lib.oracle_search.argtypes = [ctypes.c_char_p, u64, u64, u64,
                                       ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_int)]
@@ -90,6 +92,19 @@ def work_values(roots: Sequence[bytes], nonces: Sequence[int]) -> List[int]:
     out = (ctypes.c_uint64 * n)()
     _load().oracle_work_values(rb, ctypes.addressof(nn), ctypes.addressof(out), n)
     return list(out)
+
+
+def work_values_range(root: bytes, start: int, count: int, threads: Optional[int] = None):
+    """numpy uint64 array of the work values of nonces start .. start + count - 1 (mod 2^64), on
+    `threads` pthreads (default: every CPU, at most 16)."""
+    import numpy as np
+    assert len(root) == 32
+    if threads is None:
+        threads = min(16, os.cpu_count() or 1)
+    out = np.empty(count, dtype=np.uint64)
+    if count and _load().oracle_values_range(root, start & M64, count, out.ctypes.data, threads) != 0:
+        raise MemoryError("oracle_values_range allocation failed")
+    return out
 
 
 def sweep(root: bytes, threshold: int, start: int, count: int, threads: Optional[int] = None,

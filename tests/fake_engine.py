@@ -6,33 +6,101 @@ is libnanopow.so only.
 """
 import threading
 import time
+from types import SimpleNamespace
 
 import oracle
 from nanopow._lib import NPOW_CANCELLED, NPOW_EXHAUSTED, NPOW_OK, SearchResult
+
+
+class _Flag:
+    def __init__(self):
+        self.is_set = False
 
 
 class _Ticket:
     def __init__(self, fn):
         self._ev = threading.Event()
         self._res = None
+        self._info = None
 
         def run():
-            self._res = fn()
+            out = fn()
+            self._res, self._info = out if isinstance(out, tuple) else (out, None)
             self._ev.set()
         threading.Thread(target=run, daemon=True).start()
 
     def wait(self, timeout=None):
         return self._res if self._ev.wait(timeout) else None
 
+    def wait_info(self, timeout=None):
+        if not self._ev.wait(timeout):
+            return None
+        r, info = self._res, self._info
+        return info or SimpleNamespace(status=r.status, nonce=r.nonce, value=r.value, nonces_done=r.nonces_done,
+                                       winner_device=0, n_devices=1, decide_us=0.0, finish_us=0.0,
+                                       stop_after_decide_us=0.0, overshoot_nonces=0)
+
 
 class OracleEngine:
-    n_devices = 1
+    """n_devices > 1 emulates the pool's multi-device split: a search over a mask of G devices runs G
+    threads on the disjoint strides start + k * 2^64 / G, the first win stopping the others."""
 
-    def __init__(self, chunk=1 << 12, delay=0.0):
+    def __init__(self, chunk=1 << 12, delay=0.0, n_devices=1):
         self.chunk = chunk
         self.delay = delay
+        self.n_devices = n_devices
         self.calls = []
         self.lock = threading.Lock()
+        self._stats = [dict(nonces=0, launches=0, kernel_ms=0.0) for _ in range(n_devices)]
+
+    def stats(self, device=0):
+        st = self._stats[device]
+        return SimpleNamespace(kernel_ms=st["kernel_ms"], nonces=st["nonces"], launches=st["launches"],
+                               clock_mhz=0.0, early_finishes=0, kills_relayed=0, host_cpu_ms=0.0,
+                               host_wall_ms=1.0)
+
+    def reset_stats(self, device=0):
+        self._stats[device] = dict(nonces=0, launches=0, kernel_ms=0.0)
+
+    def _split(self, root, threshold, start, device_mask, cancel):
+        devs = [d for d in range(self.n_devices) if device_mask == 0 or (device_mask >> d) & 1]
+        G = len(devs)
+        spacing = (1 << 64) // G
+        stop = _Flag()
+        out = [None] * G
+        t0 = time.perf_counter()
+        decided = [None]
+
+        def run(k):
+            t = time.perf_counter()
+            r = self.search(root, threshold, (start + k * spacing) % (1 << 64), cancel=_Either(stop, cancel))
+            with self.lock:
+                st = self._stats[devs[k]]
+                st["nonces"] += r.nonces_done
+                st["launches"] += 1
+                st["kernel_ms"] += (time.perf_counter() - t) * 1e3
+                if r.status == NPOW_OK and decided[0] is None:
+                    decided[0] = (k, time.perf_counter())
+                    stop.is_set = True
+            out[k] = (r, time.perf_counter())
+        ths = [threading.Thread(target=run, args=(k,)) for k in range(G)]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        done = sum(r.nonces_done for r, _ in out)
+        if decided[0] is None:
+            res = SearchResult(out[0][0].status, None, None, done)
+            return res, None
+        k, td = decided[0]
+        win = out[k][0]
+        spans = [max(0.0, (te - td) * 1e6) for j, (_, te) in enumerate(out) if j != k]
+        res = SearchResult(NPOW_OK, win.nonce, win.value, done)
+        info = SimpleNamespace(status=NPOW_OK, nonce=win.nonce, value=win.value, nonces_done=done,
+                               winner_device=devs[k], n_devices=G, decide_us=(td - t0) * 1e6,
+                               finish_us=(max(te for _, te in out) - t0) * 1e6,
+                               stop_after_decide_us=max(spans, default=0.0), overshoot_nonces=0)
+        return res, info
 
     def work_value(self, root, nonce):
         return oracle.work_value(root, nonce)
@@ -57,4 +125,15 @@ class OracleEngine:
                 time.sleep(self.delay)
 
     def submit(self, root, threshold, start=0, device_mask=0, max_nonces_per_device=0, cancel=None):
+        if self.n_devices > 1 and not max_nonces_per_device:
+            return _Ticket(lambda: self._split(root, threshold, start, device_mask, cancel))
         return _Ticket(lambda: self.search(root, threshold, start, device_mask, max_nonces_per_device, cancel))
+
+
+class _Either:
+    def __init__(self, a, b):
+        self.a, self.b = a, b
+
+    @property
+    def is_set(self):
+        return self.a.is_set or (self.b is not None and self.b.is_set)

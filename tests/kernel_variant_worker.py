@@ -1,12 +1,8 @@
-"""Child process of tests/test_gpu_kernels.py: one search / sweep kernel variant, selected at
-npow_init by the environment, checked end to end against the oracle.
+"""Child process of tests/test_gpu_kernels.py: the shipped search / sweep kernels (two 1,024-lane
+lockstep workgroups per CU: npow_pool_kernel_ls2*, npow_sweep_kernel_ls2), checked end to end
+against the oracle in a fresh process.
 
-  ls2   the default: two 1,024-lane lockstep workgroups per CU (npow_pool_kernel_ls2*,
-        npow_sweep_kernel_ls2)
-  ls1   NANOPOW_LS_GROUPS=1: one lockstep workgroup per CU (npow_pool_kernel_ls*, npow_sweep_kernel_ls)
-  seq   NANOPOW_POOL_KERNEL=seq: the round-1 kernels (npow_pool_kernel*, npow_task_kernel<kSweep>)
-
-Each runs: 24 first-win searches at receive difficulty (every result re-hashed by hashlib), 8
+It runs: 24 first-win searches at receive difficulty (every result re-hashed by hashlib), 8
 concurrent searches (one launch table with several entries), a bounded search with no hit that
 must end EXHAUSTED after exactly its nonce budget (the dense bounded mapping: a wrong mapping
 hashes some nonces twice and others never), a bounded search whose only hit lies near the end of
@@ -32,7 +28,7 @@ LOW = 0xffff000000000000
 
 def main(variant):
     eng = _lib.Engine()
-    rng = random.Random({"ls2": 1, "ls1": 2, "seq": 3}[variant])
+    rng = random.Random(1)
     for _ in range(24):
         root = bytes(rng.getrandbits(8) for _ in range(32))
         r = eng.search(root, RECEIVE, start=rng.getrandbits(64), device_mask=1)
@@ -58,7 +54,8 @@ def main(variant):
     got = eng.sweep(root, LOW, 5, 1 << 26, device_mask=1)
     want = oracle.sweep(root, LOW, 5, 1 << 26, threads=16)
     assert got == want, (len(got), len(want))
-    print(json.dumps({"variant": variant, "ok": True, "sweep_hits": len(got)}))
+    print(json.dumps({"variant": variant, "ok": True, "sweep_hits": len(got),
+                      "pool_groups": int(eng.stats(0).pool_groups)}))
 
 
 if __name__ == "__main__":

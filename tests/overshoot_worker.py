@@ -1,0 +1,61 @@
+"""Child process of tests/test_gpu_multidevice.py: first-found cancellation across devices
+(north_star; the work_cancel -> {"error": "Cancelled"} semantics of nano-work-server.exe @1673856,
+client/work_handler.py:61-80).  Run with NANOPOW_VIRTUAL_DEVICES=G: searches split over all G
+devices (disjoint strides); for each, npow_wait_info reports when the host accepted the winner and
+how long the other devices kept hashing after that (host-observed upper bound) with the nonces that
+span is worth at each device's kernel rate.  Asserts a valid winner every time and a bound on the
+overshoot; prints one JSON line with the distributions."""
+import json
+import os
+import random
+import statistics
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(ROOT, "nano-dpow_amd"))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+
+import oracle  # noqa: E402  (the checker)
+from nanopow import _lib  # noqa: E402
+
+THRESHOLDS = {"send": 0xfffffff800000000, "receive": 0xfffffe0000000000}
+
+
+def pct(xs, p):
+    xs = sorted(xs)
+    return xs[min(len(xs) - 1, max(0, int(round(p / 100.0 * (len(xs) - 1)))))]
+
+
+def main(n_search, which):
+    eng = _lib.Engine()
+    G = eng.n_devices
+    thr = THRESHOLDS[which]
+    rng = random.Random(11)
+    spans, over, done, ttw, winners = [], [], [], [], []
+    for i in range(n_search):
+        root = bytes(rng.getrandbits(8) for _ in range(32))
+        t = eng.submit(root, thr, start=rng.getrandbits(64), device_mask=0)
+        info = t.wait_info(120)
+        assert info is not None and info.status == _lib.NPOW_OK, info
+        assert oracle.work_value_hashlib(root, info.nonce) == info.value >= thr
+        assert info.n_devices == G and 0 <= info.winner_device < G
+        spans.append(info.stop_after_decide_us)
+        over.append(info.overshoot_nonces)
+        done.append(info.nonces_done)
+        ttw.append(info.finish_us)
+        winners.append(info.winner_device)
+    kills = sum(eng.stats(d).kills_relayed for d in range(G))
+    res = {"ok": True, "devices": G, "threshold": which, "searches": n_search,
+           "stop_after_decide_us": {"p50": round(pct(spans, 50), 1), "p99": round(pct(spans, 99), 1),
+                                    "max": round(max(spans), 1)},
+           "overshoot_nonces": {"p50": pct(over, 50), "p99": pct(over, 99),
+                                "mean_over_nonces_done": round(sum(over) / max(1, sum(done)), 5)},
+           "finish_ms_p50": round(pct(ttw, 50) / 1e3, 3),
+           "distinct_winners": len(set(winners)), "kills_relayed": kills,
+           "mean_nonces_done": round(statistics.mean(done))}
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main(int(sys.argv[1]), sys.argv[2])

@@ -15,11 +15,11 @@ from conftest import ROOT
 pytestmark = pytest.mark.gpu
 
 SCENARIOS = {
-    "invalid": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_INVALID": "3"},
-    "hip": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_HIP": "2:3"},
-    "exhaust": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_HIP": "2:3"},
-    "allbad": {"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_FAULT_INVALID": "0,1"},
-    "init": {"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_FAULT_INIT": "2"},
+    "invalid": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_INVALID": "3", "NANOPOW_TEST_HOOKS": "1"},
+    "hip": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_HIP": "2:3", "NANOPOW_TEST_HOOKS": "1"},
+    "exhaust": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_HIP": "2:3", "NANOPOW_TEST_HOOKS": "1"},
+    "allbad": {"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_FAULT_INVALID": "0,1", "NANOPOW_TEST_HOOKS": "1"},
+    "init": {"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_FAULT_INIT": "2", "NANOPOW_TEST_HOOKS": "1"},
 }
 
 

@@ -1,9 +1,10 @@
 """GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
 
 Bit-exact throughout (integer work).  Run on an MI355X: ``pytest -m gpu``.
-Covers: every golden (root, nonce, value) triple through both GPU code paths
-(specialised per-root stream npow_values, generic per-lane npow_values_pairs);
-contiguous value ranges incl. 2^32 and 2^64 carries; every exhaustive sweep
+Covers: every golden (root, nonce, value) triple through all three GPU hash paths
+(npow_values = the stream the search and sweep kernels run, the seq stream, the generic
+per-lane-root kernel); contiguous value ranges incl. 2^32 and 2^64 carries and 2^20 / 2^24
+ranges; every exhaustive sweep
 fixture (8 roots x [0, 2^28), hashlib ranges, the range across 2^64 -> 0) and,
 at BASELINE config 3's full size, the 2^36 sweep; first-win search validity
 at the BASELINE thresholds; threshold edges; exhaustion, cancellation,
@@ -27,29 +28,57 @@ SEND, RECEIVE, LOW = 0xfffffff800000000, 0xfffffe0000000000, 0xfffff00000000000
 
 def test_native_library_is_the_hip_path(gpu_engine):
     assert "gfx950" in gpu_engine.version()
+    assert gpu_engine.abi_version() == _lib.NPOW_ABI_VERSION
     st = gpu_engine.stats(0)
-    assert st.cus >= 1 and st.grid >= st.cus
+    assert st.cus >= 1 and st.grid == 2 * st.cus and st.pool_groups == 2
 
 
-def test_golden_triples_both_gpu_paths(gpu_engine):
+PATHS = pytest.mark.parametrize("path", [_lib.NPOW_PATH_SEARCH, _lib.NPOW_PATH_SEQ], ids=["search_stream", "seq_stream"])
+
+
+@PATHS
+def test_golden_triples(gpu_engine, path):
+    """Every golden (root, nonce, value) triple (hashlib) through one hash path, one root at a time:
+    NPOW_PATH_SEARCH is the instruction stream the search and sweep kernels execute
+    (npow_values_kernel_ls2 -- the same uniform loads, barrier intervals and two workgroups per
+    CU), so its full 64-bit values are compared, not only its hit decisions."""
+    g = load_golden("work_values.json")["triples"]
+    got = [gpu_engine.values(bytes.fromhex(r), int(n, 16), 1, path=path)[0] for r, n, _ in g]
+    assert [f"{v:016x}" for v in got] == [v for _, _, v in g]
+
+
+def test_golden_triples_generic_path(gpu_engine):
+    """The same triples through the per-lane-root kernel (npow_values_pairs), in one launch."""
     g = load_golden("work_values.json")["triples"]
     roots = [bytes.fromhex(r) for r, _, _ in g]
     nonces = [int(n, 16) for _, n, _ in g]
-    want = [int(v, 16) for _, _, v in g]
-    assert gpu_engine.values_pairs(roots, nonces) == want
-    got = [gpu_engine.values(r, n, 1)[0] for r, n in zip(roots[:512], nonces[:512])]
-    assert got == want[:512]
+    assert gpu_engine.values_pairs(roots, nonces) == [int(v, 16) for _, _, v in g]
 
 
+@PATHS
 @pytest.mark.parametrize("start,count", [
-    (0, 1 << 16), (0xffffffff - 1000, 5000), ((1 << 64) - 3000, 6000), (12345, 1), (7, 65), (99, 64 * 1000 + 17)])
-def test_value_ranges_vs_oracle(gpu_engine, start, count):
+    (0, 1 << 16), (0xffffffff - 1000, 5000), ((1 << 64) - 3000, 6000), (12345, 1), (7, 65), (99, 64 * 1000 + 17),
+    ((1 << 32) - (1 << 19), 1 << 20), (0x0123456789abcdef, 1 << 20), ((1 << 64) - (1 << 19) - 3, 1 << 20)])
+def test_value_ranges_vs_oracle(gpu_engine, path, start, count):
+    """Contiguous ranges: ragged lengths (1, 65, 64k+17: partial rows and blocks), the 2^32 carry
+    into the nonce's high word and the 2^64 wrap, and 2^20-nonce ranges across both."""
     rng = random.Random(start ^ count)
     root = bytes(rng.getrandbits(8) for _ in range(32))
-    got = gpu_engine.values(root, start, count)
-    roots = [root] * count
-    want = oracle.work_values(roots, [(start + i) & M64 for i in range(count)])
-    assert got == want
+    got = gpu_engine.values_array(root, start, count, path=path)
+    want = oracle.work_values_range(root, start, count)
+    assert got.tolist() == want.tolist()
+
+
+def test_value_range_2p24_both_streams(gpu_engine):
+    """2^24 consecutive values (one full values launch) through both generated streams, equal to
+    each other and to the oracle's on every nonce."""
+    root = bytes.fromhex("E89208DD038FBB269987689621D52292AE9C35941A7484756ECCED92A65093BA")
+    start = 0x62f05417dd3fb691 - (1 << 23)
+    a = gpu_engine.values_array(root, start, 1 << 24, path=_lib.NPOW_PATH_SEARCH)
+    b = gpu_engine.values_array(root, start, 1 << 24, path=_lib.NPOW_PATH_SEQ)
+    want = oracle.work_values_range(root, start, 1 << 24)
+    assert (a == want).all() and (b == want).all()
+    assert int(a[1 << 23]) == 0xfffffff4000d3dac  # the Nano genesis work
 
 
 def test_sweep_fixtures(gpu_engine):

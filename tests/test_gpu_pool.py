@@ -61,8 +61,7 @@ def test_nonce_accounting_matches_device_counter(gpu_engine):
     # the quick jobs shared launches with the endless ones: most finished from the kernel's published
     # final count, before their launch ended (npow_kernel.hip "Early finish"), and every such count
     # equals the read-back after the launch
-    if gpu_engine.pool_kernel_groups() == 2:
-        assert st.early_finishes >= 16 and st.early_mismatches == 0, (st.early_finishes, st.early_mismatches)
+    assert st.early_finishes >= 16 and st.early_mismatches == 0, (st.early_finishes, st.early_mismatches)
 
 
 def test_bounded_ranges_exact_beside_unbounded_jobs(gpu_engine):
@@ -230,8 +229,6 @@ def test_new_jobs_join_a_running_launch_and_finish_early(gpu_engine):
     entry (no yield) and return as soon as their entry's last workgroup has left it (early finish),
     not when the busy jobs' launch ends (its iteration cap, ~65 ms here); every count the kernel
     published equals the read-back after the launch, and all nonces add up to the device's counter."""
-    if gpu_engine.pool_kernel_groups() != 2:
-        pytest.skip("early finish and dynamic entries are two-group-kernel features")
     gpu_engine.set_pool_tuning(budget_us=200_000)
     gpu_engine.reset_stats(0)
     try:

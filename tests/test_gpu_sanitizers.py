@@ -58,7 +58,7 @@ def test_device_drop_under_sanitizers(binary):
     """The fault policy's paths (a device dropped after 3 invalid results, its jobs re-strided onto
     the others) under ASan / TSan: 4 logical devices, device 1's wins corrupted, every search,
     ticket and bounded range over all devices (DRIVER_MASK=0)."""
-    env = {"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_FAULT_INVALID": "1", "DRIVER_MASK": "0"}
+    env = {"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_FAULT_INVALID": "1", "NANOPOW_TEST_HOOKS": "1", "DRIVER_MASK": "0"}
     if binary == "abi_asan_driver":
         env.update(ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", LSAN_OPTIONS="suppressions=tools/lsan.supp")
     else:

@@ -86,19 +86,50 @@ def test_device_strides_disjoint():
             assert all(b - a >= (1 << 64) // G for a, b in zip(starts, starts[1:]))
 
 
-@pytest.mark.parametrize("preset,local_rank,want", [(None, 3, "3"), ("0,1,2,3,4,5,6,7", 5, "5"),
-                                                    ("4,6", 1, "6"), ("2", 0, "2")])
-def test_bench_rank_sees_only_its_gpu(preset, local_rank, want):
-    """Under torchrun each bench.py rank must see exactly one GPU: LOCAL_RANK, or the LOCAL_RANK-th
-    entry of a device list the launcher already exported (else every rank would search on GPU 0)."""
+@pytest.mark.parametrize("env,local_rank,want", [
+    ({}, 3, {"HIP_VISIBLE_DEVICES": "3"}),                                   # nothing exported: device LOCAL_RANK
+    ({"HIP_VISIBLE_DEVICES": ""}, 2, {"HIP_VISIBLE_DEVICES": "2"}),          # empty (a GPU-less container): unset
+    ({"HIP_VISIBLE_DEVICES": "0,1,2,3,4,5,6,7"}, 5, {"HIP_VISIBLE_DEVICES": "5"}),
+    ({"HIP_VISIBLE_DEVICES": "4,6"}, 1, {"HIP_VISIBLE_DEVICES": "6"}),
+    ({"HIP_VISIBLE_DEVICES": "2"}, 0, None),                                 # already one device: kept
+    ({"CUDA_VISIBLE_DEVICES": "3"}, 3, None),                                # a launcher narrowed CUDA_...
+    ({"CUDA_VISIBLE_DEVICES": "4,5"}, 1, {"HIP_VISIBLE_DEVICES": "5"}),
+    ({"ROCR_VISIBLE_DEVICES": "6"}, 6, None),                                # ... or ROCR_: HIP sees one
+    ({"ROCR_VISIBLE_DEVICES": "1,3,5,7"}, 2, {"HIP_VISIBLE_DEVICES": "2"}),  # index into ROCR's list
+    ({"ROCR_VISIBLE_DEVICES": "1,3", "HIP_VISIBLE_DEVICES": "0,1"}, 1, {"HIP_VISIBLE_DEVICES": "1"}),
+])
+def test_rank_visibility_presets(env, local_rank, want):
+    """Under torchrun each bench.py rank must see exactly one GPU: its own if a launcher already
+    narrowed HIP_/CUDA_/ROCR_VISIBLE_DEVICES to one, else the LOCAL_RANK-th visible device."""
+    import bench
+    assert bench.rank_visibility(env, local_rank) == want
+
+
+@pytest.mark.parametrize("env,local_rank", [({"HIP_VISIBLE_DEVICES": "0,1"}, 2), ({"ROCR_VISIBLE_DEVICES": "4,5"}, 3)])
+def test_rank_visibility_too_few_devices_fails(env, local_rank):
+    import bench
+    with pytest.raises(SystemExit):
+        bench.rank_visibility(env, local_rank)
+
+
+def test_bench_rank_environment_is_applied_at_import():
+    """The rank's visibility is set when bench.py is imported, before anything can open the GPU."""
     import subprocess
-    env = {k: v for k, v in os.environ.items() if k != "HIP_VISIBLE_DEVICES"}
-    env.update(WORLD_SIZE="8", LOCAL_RANK=str(local_rank), RANK=str(local_rank))
-    if preset is not None:
-        env["HIP_VISIBLE_DEVICES"] = preset
+    env = {k: v for k, v in os.environ.items() if not k.endswith("_VISIBLE_DEVICES")}
+    env.update(WORLD_SIZE="8", LOCAL_RANK="5", RANK="5", HIP_VISIBLE_DEVICES="0,1,2,3,4,5,6,7")
     out = subprocess.run([sys.executable, "-c", "import os, bench; print(os.environ['HIP_VISIBLE_DEVICES'])"],
                          cwd=ROOT, env=env, capture_output=True, text=True, timeout=120, check=True)
-    assert out.stdout.strip() == want
+    assert out.stdout.strip() == "5"
+
+
+def test_bench_gpus_must_match_world_size():
+    """--gpus N under torchrun must equal WORLD_SIZE: a mismatch exits non-zero before any GPU work."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if not k.endswith("_VISIBLE_DEVICES")}
+    env.update(WORLD_SIZE="2", LOCAL_RANK="0", RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT="1")
+    p = subprocess.run([sys.executable, "bench.py", "--gpus", "4", "--no-cpu-baseline"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert p.returncode != 0 and "WORLD_SIZE=2" in p.stderr
 
 
 def _node_worker(rank, world, port, q):
@@ -144,3 +175,32 @@ def test_node_time_to_work_cross_rank_first_win():
     for s0, s1 in zip(got[0][1], got[1][1]):
         assert (s1 - s0) % (1 << 64) == 1 << 63
     assert set(glob.glob(pattern)) == before  # the shared file is unlinked at the end
+
+
+def test_inprocess_multi_gpu_path_with_oracle_engine():
+    """bench.py --gpus N without torchrun: N searches in flight over the pool's N-device mask, each
+    split into N disjoint strides (here the oracle stand-in emulates the split), every one returning a
+    valid winner; value = all nonces / wall, the timed searches' overshoot summarised, then one root
+    at a time over all N (node_ttw_ms)."""
+    import bench
+    import oracle
+    from fake_engine import OracleEngine
+    eng = OracleEngine(chunk=1 << 10, n_devices=2)
+    thr = 0xfff0000000000000
+    nonces, wall, ttw, recs, kern_ms, kern_nonces, launches, ks = bench.run_timed_inprocess(eng, 2, 4, 1, thr=thr)
+    assert len(ttw) == 8 and nonces == sum(r[1] for r in recs) and nonces == kern_nonces > 0
+    line = bench.result_line(2, 4, 1, nonces, wall, ttw, kern_ms, kern_nonces, launches, parallelism="in-process x2")
+    assert line["n_gpus"] == 2 and line["config"]["searches_total"] == 8
+    assert line["value"] == round(nonces / wall / 1e9, 4)
+    node = bench.inprocess_node_ttw(eng, 2, 6, thr=thr)
+    assert node["n"] == 6 and node["p99"] >= node["p50"] > 0
+    assert "stop_after_decide_us" in node and "overshoot_nonces" in node
+    # the emulated split searched both strides of every root
+    starts = {}
+    for root, t, start in eng.calls:
+        starts.setdefault(root, set()).add(start)
+    assert all(len(v) == 2 for v in starts.values())
+    for root, v in starts.items():
+        a, b = sorted(v)
+        assert (b - a) % (1 << 64) == 1 << 63 or (a - b) % (1 << 64) == 1 << 63
+    assert oracle.work_value(root, 0) >= 0  # the checker is importable here
