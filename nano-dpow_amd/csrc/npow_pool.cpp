@@ -326,6 +326,8 @@ struct Slot {
     uint64_t seq, base, count;
   };
   std::vector<Issued> inflight;  // ranges handed to launches that have not completed (in order)
+  uint64_t unread = 0;           // bounded job: nonces of its completed ranges whose done shards have not
+                                 // been read back (a failed device's fail_all counts them from this)
 };
 
 struct PoolInflight {
@@ -346,6 +348,7 @@ class Worker {
   Slot slots_[kMaxSlots];
   std::deque<PoolInflight> q_;
   uint64_t seq_ = 0;  // launches issued by this worker
+  uint64_t retired_seq_ = 0;  // the last launch retire() has dropped (launches retire in order)
   uint64_t seen_version_ = ~0ull;
   int ring_ = 0;
   std::chrono::steady_clock::time_point front_start_{};  // host estimate of the running launch's start
@@ -377,7 +380,7 @@ class Worker {
   int queue_readbacks();
   int retire();
   void fail_all(const std::string& msg);
-  void push_back_locked(Slot& sl, size_t from, bool skip_done = false);
+  uint64_t push_back_locked(Slot& sl, size_t from, bool skip_done = false);
   bool launch_completed(uint64_t seq) const;
   void account_clock(int ring, uint64_t seq);
   int step();
@@ -426,6 +429,7 @@ void Worker::adopt() {
     sl.gen = ++g_gen;
     sl.win_seen = sl.requeue = sl.no_more = sl.readback = sl.fin_seen = sl.early = false;
     sl.stop_us = 0;
+    sl.unread = 0;
     sl.fresh = true;
     sl.inflight.clear();
     j->on_dev[k] = 1;
@@ -587,27 +591,32 @@ void Worker::handle_win(int s) {
 // failed): hand them back to the front of the job's queue for this device, in order.  With
 // skip_done, a range whose launch has already completed on the GPU (retire() has not seen it yet)
 // stays: it was hashed in full, and handing it back would hash it again and over-count the job's
-// nonces_done (a dropped device's check_slots / fail_all).
-void Worker::push_back_locked(Slot& sl, size_t from, bool skip_done) {
+// nonces_done (a dropped device's check_slots / fail_all).  Returns the nonces of the ranges kept.
+uint64_t Worker::push_back_locked(Slot& sl, size_t from, bool skip_done) {
   Job& j = *sl.job;
   std::vector<Slot::Issued> keep(sl.inflight.begin(), sl.inflight.begin() + (ptrdiff_t)from);
+  uint64_t kept = 0;
   for (size_t i = sl.inflight.size(); i > from; --i) {
     const Slot::Issued& r = sl.inflight[i - 1];
     if (skip_done && launch_completed(r.seq)) {
       keep.insert(keep.begin() + (ptrdiff_t)from, r);
+      kept += r.count;
       continue;
     }
     j.todo[sl.k].push_front({r.base, r.count});
   }
   sl.inflight.swap(keep);
+  return kept;
 }
 
-// The launch with sequence number seq has completed on the GPU (its stop event has fired, or
-// retire() already dropped it).
+// The launch with sequence number seq has completed on the GPU: retire() has dropped it, or its
+// stop event has fired.  A launch whose issue failed (its ranges were assigned, then the HIP call
+// failed: never in q_) has not.
 bool Worker::launch_completed(uint64_t seq) const {
+  if (seq <= retired_seq_) return true;
   for (const PoolInflight& f : q_)
     if (f.seq == seq) return hipEventQuery(d_.ev_stop[f.ring]) == hipSuccess;
-  return true;
+  return false;
 }
 
 // The launch's in-kernel clock records (PoolClk, one per XCD) into the device statistics.
@@ -822,6 +831,8 @@ int Worker::retire() {
       if (win_published(s)) handle_win(s);
       size_t m = 0;
       while (m < sl.inflight.size() && sl.inflight[m].seq <= seq) ++m;
+      if (sl.job && sl.job->max_per_dev)  // dense bounded ranges, hashed in full (fail_all's accounting)
+        for (size_t i = 0; i < m; ++i) sl.unread += sl.inflight[i].count;
       sl.inflight.erase(sl.inflight.begin(), sl.inflight.begin() + (ptrdiff_t)m);
     }
     if (g_trace_lat)
@@ -829,6 +840,7 @@ int Worker::retire() {
         if (sl.state == SlotState::kDraining && sl.job && sl.job->t_win != 0 && sl.job->t_kend == 0)
           sl.job->t_kend = now_us();
     NPOW_DBG("nanopow[%d]: launch %llu done\n", d_.id, (unsigned long long)q_.front().seq);
+    retired_seq_ = q_.front().seq;
     q_.pop_front();
     front_start_ = std::chrono::steady_clock::now();  // the next one (if any) has just started
   }
@@ -889,7 +901,12 @@ void Worker::fail_all(const std::string& msg) {
   }
   for (Slot& sl : slots_) {
     if (sl.state == SlotState::kFree) continue;
-    if (sl.job->max_per_dev) push_back_locked(sl, 0, true);
+    if (sl.job->max_per_dev) {
+      // no read-back from a failed device: the job counts its bounded ranges that completed here
+      // (each hashed in full, dense) from their sizes; the rest go back to it and are re-strided
+      const uint64_t kept = push_back_locked(sl, 0, true);
+      if (!sl.early) sl.job->done += sl.unread + kept;
+    }
     abandon_locked(sl.job, sl.k, d_.dead_code, d_.dead_msg);
     sl.job.reset();
     sl.inflight.clear();

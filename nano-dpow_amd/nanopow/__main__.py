@@ -46,22 +46,26 @@ def parse_args(argv=None) -> argparse.Namespace:
     return ap.parse_args(argv)
 
 
+LS_LANES = 1024  # lanes per workgroup of the search kernel (npow_pool_kernel_ls2*: 16 waves of 64)
+
+
 def apply_threads(eng, gpus) -> int:
     """Honour THREADS of ``--gpu P:D:THREADS``: the reference hashes THREADS nonces per kernel launch
-    (nano-work-server.exe @1681064).  Here a search launch hashes up to grid lanes x iterations
-    nonces and ends on a time budget, so THREADS is applied as a lower bound: the iteration cap
-    is raised until one launch can hold THREADS nonces (at most 65,536 iterations); below that
-    it changes nothing.  Returns the iteration cap in force (0 = left as it was)."""
-    iters = 0
+    (nano-work-server.exe @1681064).  Here a search launch of the default cap hashes up to grid x
+    1,024 lanes x cap / 2 nonces (two lockstep workgroups per CU: a launch runs half the cap in wave
+    iterations, npow_internal.h PoolShape::launch_iters) and ends on a time budget, so THREADS is
+    applied as a lower bound: the cap is raised until one launch can hold THREADS nonces (at most
+    65,536); below that it changes nothing.  Returns the cap in force (0 = left as it was)."""
+    cap = 0
     for _platform, device, threads in gpus:
-        lanes = eng.stats(device).grid * 256
+        lanes = eng.stats(device).grid * LS_LANES
         if lanes > 0:
-            iters = max(iters, -(-threads // lanes))
-    if iters > 8192:  # the engine's default cap: 2^31 nonces per launch on 256 CUs
-        iters = min(iters, 65536)
-        eng.set_tuning(iters, 0, 0)
-        logging.info("THREADS: search launches capped at %d wave iterations", iters)
-        return iters
+            cap = max(cap, 2 * -(-threads // lanes))
+    if cap > 8192:  # the engine's default cap: 2^31 nonces per launch on 256 CUs
+        cap = min(cap, 65536)
+        eng.set_tuning(cap, 0, 0)
+        logging.info("THREADS: search launches capped at %d (%d wave iterations per launch)", cap, cap // 2)
+        return cap
     return 0
 
 

@@ -20,14 +20,19 @@ SCENARIOS = {
     "exhaust": {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_FAULT_HIP": "2:3", "NANOPOW_TEST_HOOKS": "1"},
     "allbad": {"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_FAULT_INVALID": "0,1", "NANOPOW_TEST_HOOKS": "1"},
     "init": {"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_FAULT_INIT": "2", "NANOPOW_TEST_HOOKS": "1"},
+    "hooks_off": {"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_FAULT_INVALID": "0,1", "NANOPOW_FAULT_INIT": "0"},
 }
 
 
 @pytest.mark.parametrize("scenario", sorted(SCENARIOS))
 def test_fault_scenario(scenario):
     env = dict(os.environ, **SCENARIOS[scenario])
+    if "NANOPOW_TEST_HOOKS" not in SCENARIOS[scenario]:
+        env.pop("NANOPOW_TEST_HOOKS", None)
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "fault_worker.py"), scenario], env=env,
                        capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
     assert out["ok"] and out["scenario"] == scenario
+    if scenario == "hooks_off":
+        assert "ignored" in p.stderr and "TEST HOOKS ACTIVE" not in p.stderr

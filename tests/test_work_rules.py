@@ -70,11 +70,14 @@ def test_gpu_threads_is_a_lower_bound_on_the_launch():
             self.tuning = None
 
         def stats(self, device):
-            return type("S", (), {"grid": 1024})()  # 256 CUs x 4 workgroups: 262,144 lanes
+            return type("S", (), {"grid": 512})()  # 256 CUs x 2 workgroups of 1,024 lanes: 524,288 lanes
 
         def set_tuning(self, iters, poll, blocks):
             self.tuning = iters
     e = Stub()
-    assert apply_threads(e, [(0, 0, 1048576)]) == 0 and e.tuning is None   # the default: 4 iterations' worth
+    assert apply_threads(e, [(0, 0, 1048576)]) == 0 and e.tuning is None   # the default: 2 iterations' worth
+    # a launch of cap c runs c / 2 wave iterations of 524,288 lanes: 2^32 nonces need 8,192 of them
     assert apply_threads(e, [(0, 0, 1 << 32)]) == 16384 and e.tuning == 16384
+    assert apply_threads(e, [(0, 0, (1 << 32) + 1)]) == 16386
+    assert apply_threads(e, [(0, 0, 1 << 31)]) == 0                       # exactly the default launch
     assert apply_threads(e, [(0, 0, 1 << 40)]) == 65536                   # capped
