@@ -1334,6 +1334,10 @@ def main_inprocess(eng, args) -> int:
     if clk:
         line["sysfs_sclk_mhz"] = clk
     line["timed_overshoot"] = overshoot_summary([r[2] for r in recs], [r[3] for r in recs], [r[1] for r in recs])
+    if os.environ.get("NANOPOW_VIRTUAL_DEVICES"):
+        line["virtual_devices_note"] = (f"NANOPOW_VIRTUAL_DEVICES: the {n} devices are logical ones time-sharing one "
+                                        "GPU; their launches overlap, so per-device kernel times, the roofline and "
+                                        "the overshoot spans are not those of separate GPUs (a rehearsal of the path)")
     line["early_finishes"] = sum(k.early_finishes for k in ks)
     line["kills_relayed"] = sum(k.kills_relayed for k in ks)
     if args.node_searches:

@@ -382,6 +382,7 @@ class Worker {
   void fail_all(const std::string& msg);
   uint64_t push_back_locked(Slot& sl, size_t from, bool skip_done = false);
   bool launch_completed(uint64_t seq) const;
+  bool launch_started(uint64_t seq) const;
   void account_clock(int ring, uint64_t seq);
   int step();
   void nap();
@@ -609,6 +610,15 @@ uint64_t Worker::push_back_locked(Slot& sl, size_t from, bool skip_done) {
   return kept;
 }
 
+// The launch with sequence number seq has begun on the GPU: retired, or the start event recorded
+// right before it on the stream has fired (the launches ahead of it are done).
+bool Worker::launch_started(uint64_t seq) const {
+  if (seq <= retired_seq_) return true;
+  for (const PoolInflight& f : q_)
+    if (f.seq == seq) return hipEventQuery(d_.ev_start[f.ring]) == hipSuccess;
+  return false;
+}
+
 // The launch with sequence number seq has completed on the GPU: retire() has dropped it, or its
 // stop event has fired.  A launch whose issue failed (its ranges were assigned, then the HIP call
 // failed: never in q_) has not.
@@ -625,8 +635,13 @@ void Worker::account_clock(int ring, uint64_t seq) {
   for (int x = 0; x < kClkWaves; ++x) {
     const PoolClk& c = d_.pmb->clk[ring][x];
     if (__atomic_load_n(&c.seq, __ATOMIC_ACQUIRE) != (uint32_t)seq) continue;
-    cyc += (double)__atomic_load_n(&c.cycles, __ATOMIC_RELAXED);
-    ref += (double)__atomic_load_n(&c.ref, __ATOMIC_RELAXED);
+    const double cy = (double)__atomic_load_n(&c.cycles, __ATOMIC_RELAXED);
+    const double rf = (double)__atomic_load_n(&c.ref, __ATOMIC_RELAXED);
+    // a record from a wave that ran for a few ticks only (a launch that found its job already over) is
+    // too coarse to price, and a clock outside 0.3-4 GHz is not a clock: skip both
+    if (rf < 1000.0 || cy < 3.0 * rf || cy > 40.0 * rf) continue;
+    cyc += cy;
+    ref += rf;
   }
   std::lock_guard<std::mutex> sg(d_.stats_mu);
   d_.clk_ticks += cyc;
@@ -681,10 +696,17 @@ void Worker::check_slots() {
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);
       sl.state = SlotState::kDraining;
     } else if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {
-      if (!j.decided.load()) {
+      bool started = false;  // has any launch holding the job begun on the GPU?
+      for (const Slot::Issued& r : sl.inflight) started = started || launch_started(r.seq);
+      {
         std::lock_guard<std::mutex> g(g_pool.mu);
-        j.cancel_req = true;
-        decide_locked(j, NPOW_CANCELLED);
+        if (!j.decided.load()) {
+          j.cancel_req = true;
+          decide_locked(j, NPOW_CANCELLED);
+        }
+        // queued behind another launch only: this device hashes nothing of the job after the decision
+        // (a one-job launch starting after the kill leaves at once; others see it within an iteration)
+        if (!started && j.t_decide > 0 && j.t_stop[sl.k] == 0) j.t_stop[sl.k] = j.t_decide;
       }
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);  // in-flight waves stop
       sl.state = SlotState::kDraining;
