@@ -418,15 +418,10 @@ __device__ __forceinline__ void ls2_kill(PoolDevState* st, PoolMailbox* mb, uint
   if (counted && ls2_empty(st, slot)) ls2_publish_fin(st, mb, slot, gen);
 }
 
-// The host raised the entry's kill word (a cancel, or another device won the job).
-__device__ __forceinline__ bool ls2_killed(const PoolMailbox* mb, uint32_t slot, uint64_t gen) {
-  return __hip_atomic_load(&mb->kill[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == gen;
-}
-
 // Join it unless it is over (then leave again at once, without hashing).  Uncounted launches
-// (PoolTable::counted) only check that it is live.  (The kill word is not read here: the extra load
-// in ls2_pick, a call, made the search loop reload 3 more spilled SGPRs with v_readlane every
-// iteration; a counted launch's polls see a kill within an iteration anyway.)
+// (PoolTable::counted) only check that it is live.  (The pinned kill word is not read here: the extra
+// load in ls2_pick, a call, made the search loop reload 3 more spilled SGPRs with v_readlane every
+// iteration; the polls see a kill within an iteration anyway.)
 __device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen, bool counted) {
   if (!counted) return load_dead(st, slot) < gen;
   __hip_atomic_fetch_add(&st->count[slot][ls2_shard()].wgs, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -624,12 +619,11 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     if (counted) {
       first = ls2_pick(tab, st, mb, g % n, true, &s_seen);
     } else {
-      // a one-job launch that starts after the host raised the job's kill word (another device won it,
-      // or it was cancelled, while this launch was queued) relays the kill and hashes nothing
+      // only the device-side dead word: reading the pinned kill word here too (512 workgroups' PCIe reads
+      // at once) delayed every launch's first hash by 30-60 us -- receive-difficulty searches p50 0.29-0.33
+      // against 0.26 ms (profiles/r03_ab_latency.jsonl); a kill is seen by the first polls instead
       ConstEntry* pe = ls2_entry(tab, mb, g % n);
-      const bool killed = ls2_killed(mb, pe->slot, pe->gen);
-      if (killed && lane == 0) ls2_kill(st, mb, pe->slot, pe->gen, false);
-      first = (!killed && load_dead(st, pe->slot) < pe->gen) ? g % n : kNoEntry;
+      first = load_dead(st, pe->slot) < pe->gen ? g % n : kNoEntry;
     }
     if (lane == 0) s_next = first;
   }

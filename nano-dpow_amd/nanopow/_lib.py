@@ -166,14 +166,17 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         lib.npow_pool_status.restype = ctypes.c_int
         lib.npow_set_pool_tuning.argtypes = [u32, u32]
         lib.npow_set_pool_tuning.restype = ctypes.c_int
-        lib.npow_values_path.argtypes = [ctypes.c_int, u8p, u64, u64, ctypes.c_int, p]
-        lib.npow_values_path.restype = ctypes.c_int
-        lib.npow_wait_info.argtypes = [u64, ctypes.c_int64, ctypes.POINTER(SearchInfo)]
-        lib.npow_wait_info.restype = ctypes.c_int
-        lib.npow_device_stats_get_sized.argtypes = [ctypes.c_int, ctypes.POINTER(DeviceStats), u64]
-        lib.npow_device_stats_get_sized.restype = ctypes.c_int
-        lib.npow_abi_version.argtypes = []
-        lib.npow_abi_version.restype = ctypes.c_int
+        # ABI 3 (a library of an earlier revision, e.g. an A/B build of round-2 sources, lacks them:
+        # stats() then falls back to npow_device_stats_get, whose struct is a prefix of DeviceStats)
+        if hasattr(lib, "npow_abi_version"):
+            lib.npow_values_path.argtypes = [ctypes.c_int, u8p, u64, u64, ctypes.c_int, p]
+            lib.npow_values_path.restype = ctypes.c_int
+            lib.npow_wait_info.argtypes = [u64, ctypes.c_int64, ctypes.POINTER(SearchInfo)]
+            lib.npow_wait_info.restype = ctypes.c_int
+            lib.npow_device_stats_get_sized.argtypes = [ctypes.c_int, ctypes.POINTER(DeviceStats), u64]
+            lib.npow_device_stats_get_sized.restype = ctypes.c_int
+            lib.npow_abi_version.argtypes = []
+            lib.npow_abi_version.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -414,7 +417,10 @@ class Engine:
 
     def stats(self, device: int = 0) -> DeviceStats:
         s = DeviceStats()
-        _check(self.lib.npow_device_stats_get_sized(device, ctypes.byref(s), ctypes.sizeof(s)), self.lib)
+        if hasattr(self.lib, "npow_device_stats_get_sized"):
+            _check(self.lib.npow_device_stats_get_sized(device, ctypes.byref(s), ctypes.sizeof(s)), self.lib)
+        else:
+            _check(self.lib.npow_device_stats_get(device, ctypes.byref(s)), self.lib)
         return s
 
     def abi_version(self) -> int:
