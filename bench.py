@@ -1027,19 +1027,24 @@ def _http_ttw(eng, n, thr=SEND, base=30_000_000, device_mask=1):
     return out
 
 
-def fixed_overhead(eng, mask: int, n: int = 200):
-    """The per-search cost that does not scale with nonces: searches at threshold 0 (every nonce
-    wins, so the first hash of the launch wins) through the C ABI, one at a time -- submit, adopt,
-    launch, one hash, the win seen and re-validated, the launch drained, the reply."""
-    ts = []
+def fixed_overhead(eng, mask: int, rate: float, n: int = 300):
+    """The per-search cost that does not scale with nonces: n receive-difficulty searches (2^23 nonces
+    expected, ~0.25 ms of hashing) through the C ABI, one at a time; per search, its wall time minus
+    its nonces at the kernel rate -- submit, adopt, launch, the cold first hash, the win seen and
+    re-validated, the launch drained, the reply.  (Threshold 0 is no measure of it: every wave of the
+    first hash wins, and 8,192 win atomics on one word serialise for ~0.15 ms.)"""
+    res, ts = [], []
     for i in range(n):
         t = time.perf_counter()
-        r = eng.search(bench_root(40_000_000 + i), 0, start=bench_start(i), device_mask=mask)
-        ts.append(time.perf_counter() - t)
+        r = eng.search(bench_root(40_000_000 + i), 0xfffffe0000000000, start=bench_start(i), device_mask=mask)
+        dt = time.perf_counter() - t
         if r.status != 0:
             raise RuntimeError(f"overhead search {i} returned status {r.status}")
-    return {"p50": round(pct(ts, 50) * 1e3, 4), "mean": round(statistics.mean(ts) * 1e3, 4), "n": n,
-            "how": "npow_search at threshold 0 (the launch's first hash wins), one at a time"}
+        ts.append(dt)
+        res.append(dt - r.nonces_done / rate)
+    return {"p50": round(pct(res, 50) * 1e3, 4), "mean": round(statistics.mean(res) * 1e3, 4), "n": n,
+            "receive_p50_ms": round(pct(ts, 50) * 1e3, 4),
+            "how": "receive-difficulty searches (fffffe00...) one at a time: wall time - nonces_done / kernel rate"}
 
 
 def latency_sample(eng, dev: int, n: int, rate_gnps=None):
@@ -1057,12 +1062,12 @@ def latency_sample(eng, dev: int, n: int, rate_gnps=None):
             raise RuntimeError(f"latency search {i} returned status {r.status}")
         nn.append(r.nonces_done)
     wall = time.perf_counter() - t0
-    over = fixed_overhead(eng, 1 << dev)
     E = float(1 << 29)
     ln2 = 0.6931471805599453
     mean_n = statistics.mean(nn)
     se_n = statistics.stdev(nn) / n ** 0.5 if n > 1 else 0.0
     rate = (rate_gnps or sum(nn) / wall / 1e9) * 1e9  # nonces / s
+    over = fixed_overhead(eng, 1 << dev, rate)
     oh = over["p50"] * 1e-3
     out = {"p50": round(pct(ttw, 50) * 1e3, 3), "p99": round(pct(ttw, 99) * 1e3, 3),
            "mean": round(statistics.mean(ttw) * 1e3, 3), "n": n, "gnps": round(sum(nn) / wall / 1e9, 4),
