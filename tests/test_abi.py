@@ -76,17 +76,28 @@ def test_init_without_gpu_reports_no_device():
         _lib.Engine()
 
 
-def test_device_stats_layout_matches_header(tmp_path):
-    """The ctypes mirror of npow_device_stats (_lib.DeviceStats) has the C struct's size and field
-    offsets: compiled from include/nanopow.h with gcc and compared field by field."""
-    fields = [f for f, _ in _lib.DeviceStats._fields_]
+@pytest.mark.parametrize("cname,pytype", [("npow_device_stats", "DeviceStats"), ("npow_search_info", "SearchInfo")])
+def test_struct_layout_matches_header(tmp_path, cname, pytype):
+    """The ctypes mirrors of npow_device_stats and npow_search_info (_lib.DeviceStats, _lib.SearchInfo)
+    have the C structs' sizes and field offsets: compiled from include/nanopow.h with gcc and compared
+    field by field."""
+    cls = getattr(_lib, pytype)
+    fields = [f for f, _ in cls._fields_]
     src = tmp_path / "layout.c"
     src.write_text('#include <stddef.h>\n#include <stdio.h>\n#include "nanopow.h"\nint main(void) {\n'
-                   '  printf("%zu\\n", sizeof(npow_device_stats));\n'
-                   + "".join(f'  printf("%zu\\n", offsetof(npow_device_stats, {f}));\n' for f in fields)
+                   f'  printf("%zu\\n", sizeof({cname}));\n'
+                   + "".join(f'  printf("%zu\\n", offsetof({cname}, {f}));\n' for f in fields)
                    + "  return 0;\n}\n")
     exe = tmp_path / "layout"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), "-o", str(exe), str(src)], check=True)
     vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
-    assert vals[0] == ctypes.sizeof(_lib.DeviceStats)
-    assert vals[1:] == [getattr(_lib.DeviceStats, f).offset for f in fields]
+    assert vals[0] == ctypes.sizeof(cls)
+    assert vals[1:] == [getattr(cls, f).offset for f in fields]
+
+
+def test_abi_version_constant_matches_header():
+    txt = open(os.path.join(ROOT, "include", "nanopow.h")).read()
+    assert re.search(r"#define NPOW_ABI_VERSION (\d+)", txt).group(1) == str(_lib.NPOW_ABI_VERSION)
+    for name in ("NPOW_PATH_SEARCH", "NPOW_PATH_SEQ", "NPOW_PATH_GENERIC"):
+        assert int(re.search(rf"#define {name} (\d+)", txt).group(1)) == getattr(_lib, name)
+    assert _lib.load().npow_abi_version() == _lib.NPOW_ABI_VERSION

@@ -253,3 +253,31 @@ def test_stats_count_every_nonce(gpu_engine):
     gpu_engine.sweep(bytes(32), SEND, 0, 10_000_019)
     st = gpu_engine.stats(0)
     assert st.nonces == 10_000_019 and st.launches >= 1 and st.kernel_ms > 0
+
+
+def test_abi2_stats_call_writes_only_its_prefix(gpu_engine):
+    """npow_device_stats_get (the ABI-2 call) writes the struct only up to dyn_entries, as a caller
+    compiled against the round-2 header allocates it; npow_device_stats_get_sized writes what it is
+    told (the struct grew while the call kept its signature)."""
+    import ctypes
+    lib = gpu_engine.lib
+    buf = (ctypes.c_uint8 * ctypes.sizeof(_lib.DeviceStats))(*([0xA5] * ctypes.sizeof(_lib.DeviceStats)))
+    prefix = _lib.DeviceStats.kills_relayed.offset
+    assert lib.npow_device_stats_get(0, ctypes.cast(buf, ctypes.POINTER(_lib.DeviceStats))) == 0
+    assert bytes(buf[prefix:]) == b"\xa5" * (len(buf) - prefix)
+    assert lib.npow_device_stats_get_sized(0, ctypes.cast(buf, ctypes.POINTER(_lib.DeviceStats)), 16) == 0
+    assert bytes(buf[prefix:]) == b"\xa5" * (len(buf) - prefix)
+    st = gpu_engine.stats(0)
+    assert st.pool_groups == 2 and st.cus > 0
+
+
+def test_wait_info_single_device(gpu_engine):
+    """npow_wait_info on a one-device search: the winner is that device, the decision precedes the
+    finish, no other device to overshoot; the result re-validates under hashlib."""
+    root = bytes(range(100, 132))
+    info = gpu_engine.submit(root, RECEIVE, start=77, device_mask=1).wait_info(30)
+    assert info.status == _lib.NPOW_OK and info.winner_device == 0 and info.n_devices == 1
+    assert 0 < info.decide_us <= info.finish_us
+    assert info.stop_after_decide_us == 0 and info.overshoot_nonces == 0
+    assert oracle.work_value_hashlib(root, info.nonce) == info.value >= RECEIVE
+    assert info.nonces_done > 0
