@@ -136,18 +136,15 @@ def stream_mix(path=STREAM_INC):
     return {"valu": int(m.group(1)), "mix": mix, "executed_int32_ops": ops}
 
 
-# The generated stream's cost in a tail-free harness (informational, next to the roofline): two
-# 1,024-lane workgroups per CU, the stream loading its own uniforms (1,677 VALU instructions):
-# 4,852 SIMD cycles per wave-hash (64 nonces) in tools/experiments/stream_lockstep.py
-# (profiles/r02_stream_bound_g2.jsonl "vop2_ld").  The harness is not a strict bound: its workgroups
-# start together and stay in step, while a kernel's two groups per CU drift apart and overlap
-# better (the kernel's own cycles per hash, from its in-kernel clock, are reported beside it).
-STREAM = {"cycles": 4852, "valu": 1677, "kernel": "npow_pool_kernel_ls2_arg<false>",
-          "sweep_kernel": "npow_sweep_kernel_ls2",
-          "src": "tools/experiments/stream_lockstep.py, profiles/r02_stream_bound_g2.jsonl"}
-STREAM_CYCLES_PER_HASH = STREAM["cycles"]
-STREAM_CLOCK_GHZ = 2.39   # in-kernel s_memtime / s_memrealtime under this load
-STREAM_BOUND_GNPS = 1024 * 64 * STREAM_CLOCK_GHZ / STREAM_CYCLES_PER_HASH  # 1,024 SIMDs
+STREAM = {"kernel": "npow_pool_kernel_ls2_arg<false>", "sweep_kernel": "npow_sweep_kernel_ls2"}
+# The issue model of the shipped stream (round 3, tools/experiments/dual_issue.py): a SIMD issues one
+# half-rate instruction (v_alignbit_b32, v_lshl_add_u64) per quad-cycle, or two full-rate ones, and a
+# full-rate instruction of another wave can ride in an alignbit's shadow (not in a 64-bit add's).  The
+# quad-cycles of one 64-nonce wave-hash are then at least adds + alignbits + max(0, full - alignbits) / 2.
+def issue_bound_cycles(mix):
+    adds, aligns = mix["mix"].get("v_lshl_add_u64", 0), mix["mix"].get("v_alignbit_b32", 0)
+    full = mix["valu"] - adds - aligns
+    return 4 * (adds + aligns + max(0, full - aligns) / 2)
 # rocprofv3 PMC passes of the bench's own command (tools/pmc_bench.sh), newest first
 PMC_POOL = ("r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
 PMC_SWEEP = ("r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
@@ -618,15 +615,15 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
                          "loop VALU per wave iteration) x 64 lanes; that run's own launches (its avg_launch_ms "
                          "and clock), to compare with nonces_per_launch") if pmc_npd else None,
             "launches": launches,
-            "stream_harness": {
-                "gnps": round(STREAM_BOUND_GNPS, 3),
-                "cycles_per_hash": STREAM_CYCLES_PER_HASH,
-                "kernel_cycles_per_hash": None,  # filled in once the in-kernel clock is known (main)
-                "what": f"the generated {STREAM['valu']:,}-instruction stream in a tail-free "
-                        f"harness ({STREAM_CYCLES_PER_HASH:,} SIMD cycles per 64 nonces, i.e. {STREAM_BOUND_GNPS:.2f} "
-                        f"Gnonce/s at {STREAM_CLOCK_GHZ} GHz; {STREAM['src']}); kernel_cycles_per_hash is the "
-                        "kernel's own figure at its in-kernel clock; the roofline frac is capped by the stream's "
-                        "half-rate share (v_lshl_add_u64, v_alignbit_b32), not by the kernel around it",
+            "issue_model": {
+                "kernel_cycles_per_hash": None,  # filled in once the in-kernel clock is known (add_clock)
+                "bound_cycles_per_hash": round(issue_bound_cycles(mix) + 4 * LOOP_VALU / 2),
+                "what": "SIMD cycles per 64-nonce wave-hash: the kernel's own (1,024 SIMDs x 64 x in-kernel clock / "
+                        "kernel rate) against the issue bound of its instruction mix (one half-rate instruction "
+                        "per quad-cycle; full-rate ones in pairs or in an alignbit's shadow; "
+                        "tools/experiments/dual_issue.py).  Co-issue lets the kernel exceed one int32 op per lane "
+                        "per cycle, so frac_at_measured_sclk can pass 1; the GPU is then power-bound and lowers "
+                        "its clock (sclk_mhz)",
             },
         },
         "cpu_baseline": None,
@@ -1317,7 +1314,7 @@ def add_clock(line, clocks, over):
     kg = line["roofline"]["kernel_gnps"]
     if kg:  # SIMD cycles per 64-nonce wave-hash at the in-kernel clock (1,024 SIMDs per GPU)
         n = line["n_gpus"]
-        line["roofline"]["stream_harness"]["kernel_cycles_per_hash"] = round(1024 * 64 * mhz * 1e6 / (kg / n * 1e9), 1)
+        line["roofline"]["issue_model"]["kernel_cycles_per_hash"] = round(1024 * 64 * mhz * 1e6 / (kg / n * 1e9), 1)
 
 
 def main_inprocess(eng, args) -> int:

@@ -1040,6 +1040,33 @@ def _pair_regs(tok: str) -> List[str]:
     return [f"v{r}" for r in range(int(lo), int(hi) + 1)]
 
 
+# Round 3 (tools/experiments/dual_issue.py): a gfx950 SIMD issues one v_alignbit_b32 per quad-cycle and
+# can issue a full-rate instruction of ANOTHER wave in its shadow -- but only when the alignbit's wave
+# wins arbitration first (priority, then age); v_lshl_add_u64 hosts no full-rate op (a v_mov_b32 only).
+# insert_setprio raises a wave's priority while it runs half-rate instructions, so that a wave in its
+# full-rate run fills the shadows of another's alignbits instead of starving it.
+SETPRIO_MODES = {"h": {"A": 1, "D": 1, "F": 0}, "a": {"A": 1, "D": 0, "F": 0},
+                 "ad": {"A": 2, "D": 1, "F": 0}, "d": {"A": 0, "D": 1, "F": 0}}
+
+
+def insert_setprio(lines: List[str], mode: str) -> List[str]:
+    pr = SETPRIO_MODES[mode]
+    out, cur = [], 0
+    for ln in lines:
+        opc = ln.split(" ", 1)[0]
+        if opc.startswith("v_"):
+            cls = "A" if opc.startswith("v_alignbit") else ("D" if opc.startswith(("v_lshl_add_u64", "v_bitop3"))
+                                                            else "F")
+            want = pr[cls]
+            if want != cur:
+                out.append(f"s_setprio {want}")
+                cur = want
+        out.append(ln)
+    if cur != 0:
+        out.append("s_setprio 0")
+    return out
+
+
 def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
     regs: Dict[int, int] = {}
     named: Dict[str, int] = {"nonce_lo": nonce & M32, "nonce_hi": nonce >> 32, "k8": 1 << 8, "k16": 1 << 16,
@@ -1312,6 +1339,8 @@ def main() -> int:
     ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
     ap.add_argument("--fuse-out", choices=["bitop3", "none"], default="bitop3",
                     help="fold the output xors H0 ^ (v0 ^ v8) into v_bitop3_b32 (fuse_output_xor)")
+    ap.add_argument("--prio", choices=["none", "h", "a", "ad", "d"], default="none",
+                    help="s_setprio at instruction-class changes (round 3 experiments, insert_setprio)")
     ap.add_argument("--pad", choices=["odd", "even", "none", "odd64", "even64", "odd128", "even128"], default="odd",
                     help="placement of the stream: 4 (mod 8) [odd], 0 (mod 8) [even], or as it falls; "
                          "odd64 / even64 / odd128 / even128: 4 or 0 bytes past a 64- or 128-byte boundary")
@@ -1397,6 +1426,8 @@ def main() -> int:
             if got != want:
                 print(f"MISMATCH (uload) root={root.hex()} nonce={nonce:016x}")
                 return 1
+    if args.prio != "none":
+        lines = insert_setprio(lines, args.prio)
     host_prog = c_expr_program(frontier)
     write_inc(args.out, lines, frontier, host_prog, args.base, vmax, counts, f"{args.sched} --rotl1 {args.rotl1} --add {args.add} --enc {args.enc}"
               + (f" --rotmad {args.rotmad}" if args.rotmad != "none" else "") + (" --swapmov" if args.swapmov else "")
@@ -1405,8 +1436,10 @@ def main() -> int:
               + (f" --func {args.func}" if args.func != "npow_asm_work_value" else "")
               + (f" --uload {args.uload}" if args.uload >= 0 else "")
               + (f" --split {args.split}" if args.split != "none" else "")
+              + (f" --barrier-every {args.barrier_every}" if args.barrier_every != 1 else "")
               + (f" --base {args.base}" if args.base != 16 else "")
-              + (f" --limit {args.limit}" if args.limit != 64 else ""), est, args.func)
+              + (f" --limit {args.limit}" if args.limit != 64 else "")
+              + (f" --prio {args.prio}" if args.prio != "none" else ""), est, args.func)
     print(f"ops={len(ops)} instrs={len(lines)} {counts} uniforms={len(frontier)} vgpr_window=v{args.base}..v{vmax - 1} "
           f"est_cycles={est:.0f} checked={args.check} -> {os.path.normpath(args.out)}")
     return 0
