@@ -203,7 +203,7 @@ int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint6
 
 /* Work values of `count` consecutive nonces start, start+1, ... for one root,
  * computed by the instruction stream the search and sweep kernels execute
- * (npow_values_kernel_ls2: the same uniform loads, barrier intervals and
+ * (npow_values_kernel_ls2: the same uniform loads, priority runs and
  * workgroup shape), so the parity tests compare that stream's full 64-bit values
  * with the CPU.  device = logical device index. */
 int npow_values(int device, const uint8_t root[32], uint64_t start, uint64_t count, uint64_t* values_out);

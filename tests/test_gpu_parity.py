@@ -40,7 +40,7 @@ PATHS = pytest.mark.parametrize("path", [_lib.NPOW_PATH_SEARCH, _lib.NPOW_PATH_S
 def test_golden_triples(gpu_engine, path):
     """Every golden (root, nonce, value) triple (hashlib) through one hash path, one root at a time:
     NPOW_PATH_SEARCH is the instruction stream the search and sweep kernels execute
-    (npow_values_kernel_ls2 -- the same uniform loads, barrier intervals and two workgroups per
+    (npow_values_kernel_ls2 -- the same uniform loads, priority runs and two workgroups per
     CU), so its full 64-bit values are compared, not only its hit decisions."""
     g = load_golden("work_values.json")["triples"]
     got = [gpu_engine.values(bytes.fromhex(r), int(n, 16), 1, path=path)[0] for r, n, _ in g]
