@@ -25,6 +25,7 @@ GROUPS = int(os.environ.get("LOCKSTEP_GROUPS", "1"))
 NONCE, VLO, VHI = (6, 4, 5) if GROUPS > 1 else (100, 102, 103)
 # LOCKSTEP_SKEW=P: odd workgroups first issue P dummy xors, so the two groups of a CU start out of phase
 SKEW = int(os.environ.get("LOCKSTEP_SKEW", "0"))
+SYNC = int(os.environ.get("LOCKSTEP_SYNC", "1"))
 
 
 def bind(path):
@@ -79,7 +80,10 @@ def main():
         # one __syncthreads per hash for a stream without barriers of its own (its waves would
         # drift apart); a lockstep stream's 96 barriers already keep them together
         skew = "\\n\\t".join(["v_xor_b32_e32 v2, v3, v2"] * max(SKEW, 1))
-        sync = "" if n_bar else "__syncthreads();  // one per hash: the seq stream has none of its own"
+        # LOCKSTEP_SYNC=k (round 3): a __syncthreads after every k-th hash for a barrier-free stream
+        # (0 = never; the search kernel has one per iteration)
+        sync = "" if n_bar or SYNC == 0 else ("__syncthreads();" if SYNC == 1 else
+                                               f"if ((it % {SYNC}) == {SYNC - 1}) __syncthreads();")
         kernels.append(f'''
 __global__ __launch_bounds__(1024) void k{k}(unsigned long long* out) {{
   asm volatile("v_mov_b32 v{NONCE}, v0\\n\\tv_mov_b32 v{NONCE + 1}, 0" ::: {clob});
@@ -141,7 +145,7 @@ int main() {{
   return 0;
 }}
 '''
-    tag = f"g{GROUPS}" + (f"s{SKEW}" if SKEW else "")
+    tag = f"g{GROUPS}" + (f"s{SKEW}" if SKEW else "") + (f"y{SYNC}" if SYNC != 1 else "")
     path = os.path.join(ROOT, "build", f"stream_lockstep_{tag}.hip")
     open(path, "w").write(src)
     subprocess.run(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-o",
