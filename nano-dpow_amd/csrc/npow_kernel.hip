@@ -598,15 +598,6 @@ __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st
   return kNoEntry;  // entries died under every attempt: the workgroup is finished
 }
 
-// NPOW_LS2_EPOCH (A/B builds; 1 = every iteration): the search loop's s_barrier closes every
-// NPOW_LS2_EPOCH-th iteration only.  The verdict is then read at the top of an epoch's first iteration
-// (right after the barrier: every request of the previous epoch is in it, and none of this epoch's can
-// be -- a request follows a whole hash) and acted on at that iteration's end.
-#ifndef NPOW_LS2_EPOCH
-#define NPOW_LS2_EPOCH 1
-#endif
-constexpr uint32_t kLsEpoch = NPOW_LS2_EPOCH;
-
 template <bool BOUNDED>
 __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
                                               PoolMailbox* __restrict__ mb, const uint64_t t_start) {
@@ -658,9 +649,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     const uint64_t step = (uint64_t)c.K << 6;
     uint32_t done = 0;
     while (it < c.it_end) {
-      const bool epoch_top = kLsEpoch == 1 || it % kLsEpoch == 0;  // it is workgroup-uniform
-      const uint32_t verdict =
-          epoch_top ? __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : ~0u;
+      const uint32_t verdict = __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const uint64_t dead = __hip_atomic_load(dead_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
       const uint32_t it0 = it;  // the poll phase
@@ -712,7 +701,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
         end = (v & 1) == 0;
         break;
       }
-      if (kLsEpoch == 1 || it % kLsEpoch == 0) __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_s_barrier();
     }
     // the workgroup's count, added by wave 0 before it leaves the entry (early finish, ls2_leave):
     // one atomic and no fence per wave
