@@ -79,9 +79,10 @@ typedef struct npow_device_stats {
   int32_t dead;           /* 1 once the device has been dropped: 3 invalid results in a row
                              (nano-work-server.exe @1669144) or a failed HIP call; searches then
                              skip it and its jobs' remaining ranges move to the other devices */
-  int32_t pool_groups;    /* lockstep workgroups per CU of the search kernel: always 2
-                             (npow_pool_kernel_ls2*; revisions before ABI 3 also had 0 = seq, 1) */
-  uint64_t early_finishes;  /* jobs finished from the kernel's published final count (two-group
+  int32_t pool_groups;    /* workgroups per CU of the search kernel (npow_pool_kernel_ls2*): 4
+                             512-lane ones -- 8 waves per SIMD either way; earlier ABI-3 libraries
+                             ran 2 of 1,024 lanes, revisions before ABI 3 also had 0 = seq, 1 */
+  uint64_t early_finishes;  /* jobs finished from the kernel's published final count (search
                                kernels): a won or killed entry's count once no workgroup is left on
                                it, before the launch that held it ends */
   uint64_t early_mismatches; /* of those, counts that the read-back after the launch contradicted
@@ -221,7 +222,7 @@ int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, 
 
 /* Tuning knobs (0 keeps the current value).  iters_per_launch: the iteration cap of a
  * search launch (default 8192; a launch runs half as many wave iterations, each the time of two
- * hashes of its SIMD's other workgroup) and the span of bounded jobs' launches;
+ * hashes of another wave of its SIMD: 8 waves share it) and the span of bounded jobs' launches;
  * poll_interval: wave iterations between a wave's polls of the host kill / yield words
  * (rounded up to a power of two; 8 waves per iteration poll grid-wide at the default 1024);
  * blocks_per_cu: 256-lane workgroups per CU of the NPOW_PATH_SEQ values kernel. */
@@ -232,13 +233,13 @@ int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t 
  * jobs stop together when it runs out -- VALU issue favours a SIMD's oldest wave, so a launch
  * of a fixed iteration count would end in a tail -- and iters_per_launch is then only the cap
  * (bounded jobs always complete their dense ranges).
- * The search kernel is npow_pool_kernel_ls2*: two 1,024-lane lockstep workgroups per CU, with
+ * The search kernel is npow_pool_kernel_ls2*: four 512-lane workgroups per CU, with
  * early finish (a won or cancelled job returns from the count its last workgroup publishes, not
  * at the end of the launch that held it) and dynamic entries (an unbounded job submitted while a
  * launch with other live jobs runs joins that launch).  A running launch is ended early (a yield)
  * only when a new job cannot join it: a bounded job, a one-job launch, a launch within 3 ms of its
  * budget, or a full ring of 32 dynamic entries.
- * blocks_per_cu: must be 0 or 2 (the workgroups per CU of the search kernel are fixed). */
+ * blocks_per_cu: must be 0 or 4 (the workgroups per CU of the search kernel are fixed). */
 int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu);
 
 /* Writes the ABI-2 prefix of npow_device_stats (through dyn_entries), as callers compiled

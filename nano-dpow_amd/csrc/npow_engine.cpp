@@ -101,7 +101,7 @@ struct Inflight {
 // Launch one chunk on d's stream bracketed by timing events.
 int launch_chunk(Device& d, Mode mode, const LaunchArgs& a, int ring, uint64_t* out) {
   HIPTRY(hipEventRecord(d.ev_start[ring], d.stream));
-  // the shipped stream's kernels: two 1,024-lane workgroups per CU; the seq values kernel: 256-lane ones
+  // the shipped stream's kernels: four 512-lane workgroups per CU; the seq values kernel: 256-lane ones
   HIPTRY(launch_task(mode, mode == Mode::kValuesSeq ? grid_of(d) : ls_grid(d), d.stream, a, d.st, d.mb_dev, out));
   HIPTRY(hipEventRecord(d.ev_stop[ring], d.stream));
   return NPOW_OK;
@@ -287,7 +287,7 @@ extern "C" {
 const char* npow_last_error(void) { return t_err.c_str(); }
 
 const char* npow_version(void) {
-  return "libnanopow 0.3 (ABI 3; gfx950 HIP kernels: blake2b-64 nonce search, two lockstep workgroups per CU; "
+  return "libnanopow 0.3 (ABI 3; gfx950 HIP kernels: blake2b-64 nonce search, four 512-lane workgroups per CU, priority runs; "
          "v_lshl_add_u64 adds, v_alignbit rotations)";
 }
 
@@ -374,7 +374,7 @@ int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t 
 int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu) try {
   if (budget_us != 0xffffffffu && budget_us > 1000000) return fail(NPOW_ERR_BAD_ARGUMENT, "budget_us must be <= 1000000");
   if (blocks_per_cu != 0 && blocks_per_cu != (uint32_t)kLsGroups)
-    return fail(NPOW_ERR_BAD_ARGUMENT, "blocks_per_cu must be 0 or 2: the search kernel runs two workgroups per CU");
+    return fail(NPOW_ERR_BAD_ARGUMENT, "blocks_per_cu must be 0 or 4: the search kernel runs four workgroups per CU");
   if (budget_us != 0xffffffffu) g_budget_us = budget_us;
   return NPOW_OK;
 } catch (...) { return guard_exception(); }

@@ -82,7 +82,7 @@ extern std::atomic<uint32_t> g_blocks_per_cu;  // npow_values_kernel_seq: 256-la
 extern std::atomic<uint32_t> g_budget_us;      // pool launches: wall-clock budget per wave (0 = off)
 
 inline int grid_of(const Device& d) { return d.cus * (int)g_blocks_per_cu.load(); }  // npow_values_kernel_seq
-// Search, sweep and values launches of the shipped stream: kLsGroups 1,024-lane workgroups per CU.
+// Search, sweep and values launches of the shipped stream: kLsGroups 512-lane workgroups per CU.
 inline int ls_grid(const Device& d) { return d.cus * kLsGroups; }
 inline PoolShape pool_shape(const Device& d) { return PoolShape{ls_grid(d)}; }
 inline uint32_t poll_mask() {

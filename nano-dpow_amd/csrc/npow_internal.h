@@ -11,9 +11,12 @@
 namespace npow {
 
 constexpr int kBlock = 256;               // npow_values_kernel_seq / npow_pairs_kernel: lanes per workgroup
-constexpr int kLsWaves = 16;              // lockstep kernels: waves per workgroup (4 per SIMD) ...
-constexpr int kLsBlock = kLsWaves * 64;   // ... 1,024 lanes
-constexpr int kLsGroups = 2;              // ... two workgroups per CU: 8 waves per SIMD, 64 VGPRs each
+// Search, sweep and values kernels of the shipped stream: 8 waves per SIMD in four 512-lane
+// workgroups per CU (round 3: against two 1,024-lane ones, -0.65 % SIMD cycles per hash in searches
+// and +1.2 % sweep rate, profiles/r03_ab_wgsize*.jsonl; 256-lane ones are slower).
+constexpr int kLsWaves = 8;                // waves per workgroup (2 per SIMD) ...
+constexpr int kLsBlock = kLsWaves * 64;    // ... 512 lanes
+constexpr int kLsGroups = 4;               // ... four workgroups per CU: 8 waves per SIMD, 64 VGPRs each
 
 // One-root tasks (launch_task): npow_sweep_kernel_ls2 (kSweep), npow_values_kernel_ls2 (kValues, the
 // shipped stream), npow_values_kernel_seq (kValuesSeq, the second stream); first-win searches are
@@ -54,7 +57,7 @@ struct DevState {
   uint64_t value;           // winning value (search)
   uint32_t zero;            // always 0: the non-polling iterations' load target
   uint8_t pad1[64 - 36];
-  // Sweep work counters (rows of 16 blocks claimed so far) of the launch's 8 sub-ranges
+  // Sweep work counters (rows of kLsWaves blocks claimed so far) of the launch's 8 sub-ranges
   // (one per XCD), for each launch parity: launch k claims from claim[k & 1][*] and zeroes
   // claim[(k + 1) & 1][*] for launch k + 1 (same stream, so launch k - 1, their previous
   // user, has finished).  One cache line each: atomics on one address serialise (~18 ns
@@ -92,13 +95,13 @@ struct alignas(64) HostMailbox {
 constexpr int kMaxSlots = 64;
 constexpr int kPoolDoneShards = 32;
 
-// Nonce-index mapping of one entry (the launch's region is [base, base + count)); w = g * 16 + wave:
+// Nonce-index mapping of one entry (the launch's region is [base, base + count)); w = g * kLsWaves + wave:
 //  * unbounded (search until won/cancelled): index = (it * W + w) * 64 + lane, W = grid
 //    waves -- every (iteration, wave) pair is distinct, so workgroups that move here from a
 //    dead entry hash fresh nonces; the region spans W * iters * 64 nonces (holes allowed);
 //  * bounded (max_nonces set; must cover its range exactly once): only the entry's own
-//    workgroups (g % n == e, rank r = g / n, k_e of them) run it, index = (it * 16 k_e + 16 r +
-//    wave) * 64 + lane, dense over [0, count) with count <= 16 k_e * iters * 64; others never
+//    workgroups (g % n == e, rank r = g / n, k_e of them) run it, index = (it * 8 k_e + 8 r +
+//    wave) * 64 + lane (8 = kLsWaves), dense over [0, count) with count <= 8 k_e * iters * 64; others never
 //    enter it.
 struct PoolEntry {
   uint64_t u[NPOW_ASM_N_UNIFORMS];  // nonce-independent intermediates of the root
@@ -109,7 +112,7 @@ struct PoolEntry {
   uint32_t slot;     // device slot index (PoolDevState / PoolMailbox arrays)
   uint32_t bounded;  // 1: dense mapping over the entry's own workgroups, no migrants
 };
-static_assert(offsetof(PoolEntry, u) == 0, "the two-group kernel finds an entry from its uniforms' address");
+static_assert(offsetof(PoolEntry, u) == 0, "the search kernel finds an entry from its uniforms' address");
 struct PoolTable {
   uint32_t n;          // entries in use (1..kMaxSlots)
   uint32_t poll_mask;  // a wave reads the host kill word when ((it + w) & poll_mask) == 0
@@ -121,9 +124,9 @@ struct PoolTable {
                           // a different high half ends the launch's unbounded entries
   uint32_t ring;          // PoolMailbox::clk[ring]: this launch's clock records ...
   uint32_t seq;           // ... tagged with the launch's sequence number (low 32 bits)
-  uint32_t dyn_base;      // two-group kernels: the low half of PoolMailbox::ctl when the table was built -- the
+  uint32_t dyn_base;      // search kernels: the low half of PoolMailbox::ctl when the table was built -- the
                           // launch may also search the entries the host publishes after it
-  uint32_t counted;       // two-group kernels: workgroups are counted on their entries (early finish,
+  uint32_t counted;       // search kernels: workgroups are counted on their entries (early finish,
                           // dynamic entries).  The host sets it for tables of 2 or more entries: a
                           // launch with one entry ends with it, and counting only slows its end.
   uint32_t pad[6];
@@ -178,7 +181,7 @@ struct PoolClk {
   uint64_t cycles, ref;
   uint32_t seq, pad;
 };
-// Final nonce count of a closed entry (two-group kernels): the sum of the slot's done shards once
+// Final nonce count of a closed entry (search kernels): the sum of the slot's done shards once
 // no workgroup is left on it and none can join, so a won or killed job finishes without waiting
 // for its launch to end (the other entries may keep it running for the rest of its budget).
 struct alignas(64) PoolFin {
@@ -186,7 +189,7 @@ struct alignas(64) PoolFin {
   uint64_t total;  // the slot's done shards, summed (cumulative over its generations)
   uint8_t pad[48];
 };
-// An unbounded job adopted while a two-group launch runs joins that launch instead of ending it
+// An unbounded job adopted while a search launch runs joins that launch instead of ending it
 // (a yield): the host writes its entry at ring position p (dyn[p % kDynEntries]) and then releases
 // the low half of PoolMailbox::ctl = p + 1; the launch's entries are its table's n entries followed by positions
 // dyn_base.. of the ring, and workgroups move to a new entry as they rebalance (npow_kernel.hip).
@@ -210,7 +213,7 @@ struct PoolMailbox {
   alignas(64) PoolClk clk[4][kClkWaves];  // [launch ring][XCD] (host: kEventRing == 4)
 };
 
-// Grid of a search launch: kLsGroups 1,024-lane workgroups per CU.  A "unit" is what an entry's share
+// Grid of a search launch: kLsGroups 512-lane workgroups per CU.  A "unit" is what an entry's share
 // is counted in: a workgroup of kLsWaves waves (workgroups work on one entry at a time).
 struct PoolShape {
   int grid;  // workgroups
@@ -221,7 +224,7 @@ struct PoolShape {
     return (uint64_t)(U / n + (e < U % n ? 1u : 0u)) * kLsWaves * iters * 64;
   }
   uint64_t full(uint32_t iters) const { return (uint64_t)units() * kLsWaves * iters * 64; }
-  // The iteration cap of a launch: with two lockstep workgroups per CU a wave iteration takes as long
+  // The iteration cap of a launch: with 8 waves per SIMD a wave iteration takes as long
   // as two hashes of its SIMD's other group, so half of g_iters keeps a launch's longest duration
   // (and its nonce span) where the round-1 tuning put it.
   uint32_t launch_iters(uint32_t iters) const { return iters > 1 ? iters / 2 : 1u; }

@@ -20,7 +20,7 @@
 //    alignbit's wave wins arbitration first: the stream raises its wave's priority (s_setprio 1)
 //    for each half-rate run and drops it for each full-rate run, so the 8 waves of a SIMD interleave
 //    their runs (round 3, DESIGN.md section 4: -9 % SIMD cycles per hash).  Every kernel that runs it
-//    (search, sweep, values) has two 1,024-lane workgroups per CU (8 waves per SIMD), and every
+//    (search, sweep, values) has four 512-lane workgroups per CU (8 waves per SIMD), and every
 //    loop decision is a workgroup decision.
 //  * First-win search (npow_pool_kernel_ls2*): every live job of the device's work pool in one
 //    launch; first win per job by atomicMax on its slot's dead word, published to a host-coherent
@@ -140,8 +140,8 @@ __global__ __launch_bounds__(kBlock) void npow_values_kernel_seq(const LaunchArg
 }
 
 // ---- Sweep (npow_sweep_kernel_ls2) -----------------------------------------------------------
-// Every hit of [base, base + count): two 1,024-lane workgroups per CU.  The unit of work is a row of
-// 16 consecutive 64-nonce blocks, one per wave (block = row * 16 + wave); workgroups claim runs of
+// Every hit of [base, base + count): four 512-lane workgroups per CU.  The unit of work is a row of
+// kLsWaves (8) consecutive 64-nonce blocks, one per wave (block = row * kLsWaves + wave); workgroups claim runs of
 // rows from 8 per-XCD counters (thread 0 claims and LDS broadcasts the claim: two barriers per claim
 // of <= max_claim rows), and the stop words (the device abort word, and the pinned host abort word on
 // one claim in poll_mask + 1) are read with the claim, so a cancel lands within one claim (<= 64
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kLsBlock, 8) void npow_sweep_kernel_ls2(const Launc
 // Every value of [base, base + count), hashed by exactly the instruction stream the search and sweep
 // kernels run (npow_hash_asm_lockstep_ld.inc: the same uniform loads, the same priority runs, the
 // same two-workgroups-per-CU shape), so the parity tests compare that stream's 64-bit values with the
-// oracle -- not only its hit / no-hit decisions.  Rows of 16 blocks (one per wave) go to workgroups
+// oracle -- not only its hit / no-hit decisions.  Rows of kLsWaves blocks (one per wave) go to workgroups
 // round-robin; every wave of a workgroup runs the same number of rows (workgroup-uniform control
 // flow, as the search kernel's), and lanes past the range's end hash but do not store.
 // 8 bytes per nonce written (the only kernel with algorithmic HBM traffic), coalesced: a wave stores
@@ -325,7 +325,7 @@ __device__ __forceinline__ void lds_drain() { asm volatile("s_waitcnt lgkmcnt(0)
 // workgroups are dealt to XCDs round-robin -- reads s_memtime after its first instruction and
 // both counters after its last; 2 scalar reads and one 24-byte store per 4,096 waves.
 __device__ __forceinline__ bool clk_wave() { return blockIdx.x < (unsigned)kClkWaves && threadIdx.x < 64; }
-// The two-group kernels keep the start in LDS: a register live across the whole kernel was spilled to
+// The search kernels keep the start in LDS: a register live across the whole kernel was spilled to
 // scratch by every wave (8 bytes per lane: ~4 MB written and read back per launch, in PMC).
 __shared__ uint64_t s_clk_start;
 __device__ __forceinline__ void clk_begin_lds() {
@@ -343,7 +343,7 @@ __device__ __forceinline__ void clk_end_ls2(const PoolTable* tab, PoolMailbox* m
     __hip_atomic_store(&r->seq, tab->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
-// The search body (npow_pool_kernel_ls2*): two 1,024-lane workgroups per CU put 8 waves on every
+// The search body (npow_pool_kernel_ls2*): four 512-lane workgroups per CU put 8 waves on every
 // SIMD.  Each iteration ends with an s_barrier (round 2 also had one after every interval of the
 // stream; round 3's stream has none, its waves' priority runs interleave them instead -- DESIGN.md
 // section 4), so every wave of a workgroup hashes the same number of times and everything that ends a
@@ -366,7 +366,7 @@ __device__ __forceinline__ void clk_end_ls2(const PoolTable* tab, PoolMailbox* m
 // Early finish: a won or killed entry usually shares its launch with live ones, which keep the
 // launch running for the rest of its budget; the job's nonce count would only be read back after
 // that.  Instead wave 0 of a workgroup joins an entry (adds 1 to its shard of the slot's wgs counters) before its
-// waves hash it, and leaves it (subtracts 1) after all 16 waves have added their done counts.  An
+// waves hash it, and leaves it (subtracts 1) after all its waves have added their done counts.  An
 // entry is over once its dead word holds its generation (a win, a kill relay, a yield); a joiner
 // that then finds it dead leaves at once without hashing.  Whoever sees wgs at 0 after seeing the
 // entry dead -- the last leaver, or the marker itself -- sums the slot's done shards and publishes

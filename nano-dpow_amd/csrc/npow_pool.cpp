@@ -441,7 +441,7 @@ void Worker::adopt() {
     if (sl.new_job) adopted = true;  // a new job: worth ending a long launch for
     j->seen_dev[k] = 1;
   }
-  // Unbounded jobs join the running two-group launch as dynamic entries (no yield: the launch goes
+  // Unbounded jobs join the running launch as dynamic entries (no yield: the launch goes
   // on and workgroups move to them); a new job that cannot ends the long launch instead.
   bool waiting_new = false;
   for (int s = 0; s < kMaxSlots; ++s) {
@@ -453,7 +453,7 @@ void Worker::adopt() {
 }
 
 // Publish the job of fresh slot s as a dynamic entry of the running launch (npow_internal.h
-// PoolDynEntry; two-group kernels only): exactly one launch in flight, enough of its budget left,
+// PoolDynEntry): exactly one launch in flight, enough of its budget left,
 // not yielded, a free ring position, an unbounded job with a full region left.  Its region is taken
 // from the job's queue as launch() would, and counts as part of the running launch.  Caller holds
 // g_pool.mu (adopt()).
@@ -653,7 +653,7 @@ bool Worker::win_published(int s) const {
   return !sl.win_seen && __atomic_load_n(&d_.pmb->win[s].gen, __ATOMIC_ACQUIRE) == sl.gen;
 }
 
-// The kernel published slot s's final nonce count (two-group kernels, npow_kernel.hip "Early
+// The kernel published slot s's final nonce count (npow_kernel.hip "Early
 // finish"): no workgroup is on the entry and none can join it, so a decided job is finished now
 // instead of after the launch -- which its other entries may keep running for the rest of its
 // budget.  A yielded entry (the job is re-adopted) or an invalid win (re-armed) waits for retire().

@@ -46,19 +46,20 @@ def parse_args(argv=None) -> argparse.Namespace:
     return ap.parse_args(argv)
 
 
-LS_LANES = 1024  # lanes per workgroup of the search kernel (npow_pool_kernel_ls2*: 16 waves of 64)
+LS_CU_LANES = 2048  # lanes per CU of a search launch (npow_pool_kernel_ls2*: 8 waves of 64 per SIMD)
 
 
 def apply_threads(eng, gpus) -> int:
     """Honour THREADS of ``--gpu P:D:THREADS``: the reference hashes THREADS nonces per kernel launch
     (nano-work-server.exe @1681064).  Here a search launch of the default cap hashes up to grid x
-    1,024 lanes x cap / 2 nonces (two lockstep workgroups per CU: a launch runs half the cap in wave
+    (2,048 / pool_groups) lanes x cap / 2 nonces (8 waves per SIMD: a launch runs half the cap in wave
     iterations, npow_internal.h PoolShape::launch_iters) and ends on a time budget, so THREADS is
     applied as a lower bound: the cap is raised until one launch can hold THREADS nonces (at most
     65,536); below that it changes nothing.  Returns the cap in force (0 = left as it was)."""
     cap = 0
     for _platform, device, threads in gpus:
-        lanes = eng.stats(device).grid * LS_LANES
+        st = eng.stats(device)
+        lanes = st.grid * (LS_CU_LANES // max(st.pool_groups, 1))
         if lanes > 0:
             cap = max(cap, 2 * -(-threads // lanes))
     if cap > 8192:  # the engine's default cap: 2^31 nonces per launch on 256 CUs

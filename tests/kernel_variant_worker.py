@@ -1,5 +1,5 @@
-"""Child process of tests/test_gpu_kernels.py: the shipped search / sweep kernels (two 1,024-lane
-lockstep workgroups per CU: npow_pool_kernel_ls2*, npow_sweep_kernel_ls2), checked end to end
+"""Child process of tests/test_gpu_kernels.py: the shipped search / sweep kernels (four 512-lane
+workgroups per CU: npow_pool_kernel_ls2*, npow_sweep_kernel_ls2), checked end to end
 against the oracle in a fresh process.
 
 It runs: 24 first-win searches at receive difficulty (every result re-hashed by hashlib), 8

@@ -24,4 +24,4 @@ def test_shipped_kernels_end_to_end():
                        capture_output=True, text=True, timeout=110)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
-    assert out["ok"] and out["variant"] == "ls2" and out["pool_groups"] == 2
+    assert out["ok"] and out["variant"] == "ls2" and out["pool_groups"] == 4

@@ -30,7 +30,7 @@ def test_native_library_is_the_hip_path(gpu_engine):
     assert "gfx950" in gpu_engine.version()
     assert gpu_engine.abi_version() == _lib.NPOW_ABI_VERSION
     st = gpu_engine.stats(0)
-    assert st.cus >= 1 and st.grid == 2 * st.cus and st.pool_groups == 2
+    assert st.cus >= 1 and st.grid == 4 * st.cus and st.pool_groups == 4
 
 
 PATHS = pytest.mark.parametrize("path", [_lib.NPOW_PATH_SEARCH, _lib.NPOW_PATH_SEQ], ids=["search_stream", "seq_stream"])
@@ -268,7 +268,7 @@ def test_abi2_stats_call_writes_only_its_prefix(gpu_engine):
     assert lib.npow_device_stats_get_sized(0, ctypes.cast(buf, ctypes.POINTER(_lib.DeviceStats)), 16) == 0
     assert bytes(buf[prefix:]) == b"\xa5" * (len(buf) - prefix)
     st = gpu_engine.stats(0)
-    assert st.pool_groups == 2 and st.cus > 0
+    assert st.pool_groups == 4 and st.cus > 0
 
 
 def test_wait_info_single_device(gpu_engine):

@@ -70,7 +70,7 @@ def test_gpu_threads_is_a_lower_bound_on_the_launch():
             self.tuning = None
 
         def stats(self, device):
-            return type("S", (), {"grid": 512})()  # 256 CUs x 2 workgroups of 1,024 lanes: 524,288 lanes
+            return type("S", (), {"grid": 1024, "pool_groups": 4})()  # 256 CUs x 4 workgroups of 512 lanes: 524,288 lanes
 
         def set_tuning(self, iters, poll, blocks):
             self.tuning = iters
