@@ -58,7 +58,7 @@ extern "C" {
 
 /* Hash paths of npow_values_path. */
 #define NPOW_PATH_SEARCH 0  /* the instruction stream the search and sweep kernels execute
-                               (npow_hash_asm_lockstep_ld.inc, two lockstep workgroups per CU) */
+                               (npow_hash_asm_lockstep_ld.inc, four 512-lane workgroups per CU) */
 #define NPOW_PATH_SEQ 1     /* a second generated stream, scheduled without barriers (npow_hash_asm.inc) */
 #define NPOW_PATH_GENERIC 2 /* plain HIP C++ of the 12 rounds, one (root, nonce) per lane */
 
@@ -88,7 +88,7 @@ typedef struct npow_device_stats {
   uint64_t early_mismatches; /* of those, counts that the read-back after the launch contradicted
                                (always 0: a protocol check) */
   uint64_t yields;          /* running launches ended early so that new jobs could start */
-  uint64_t dyn_entries;     /* jobs that joined a running two-group launch instead (no yield) */
+  uint64_t dyn_entries;     /* jobs that joined a running launch instead (no yield) */
   /* ---- ABI 3 (npow_device_stats_get_sized only) ---- */
   uint64_t kills_relayed;   /* losing jobs of this device stopped by another device's win: the deciding
                                thread raised this device's kill word directly (no wait for its worker) */
