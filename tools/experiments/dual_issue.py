@@ -11,6 +11,7 @@ SIMD-cycle for each half.
 
   python3 tools/experiments/dual_issue.py build      -> build/dual_issue (hipcc, gfx950)
   build/dual_issue [budget_us]                       -> one JSON line per pair (GPU box)
+DUAL_PAIRS=DA,DP,... picks the pairs, DUAL_TAG=name suffixes the binary (round 3: the reverse orders).
 """
 import os
 import subprocess
@@ -18,8 +19,9 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(os.path.dirname(HERE))
-SRC = os.path.join(ROOT, "build", "dual_issue_%s.hip" % os.environ.get("DUAL_SPLIT", "half"))
-BIN = os.path.join(ROOT, "build", "dual_issue_%s" % os.environ.get("DUAL_SPLIT", "half"))
+TAG = os.environ.get("DUAL_SPLIT", "half") + ("_" + os.environ["DUAL_TAG"] if os.environ.get("DUAL_TAG") else "")
+SRC = os.path.join(ROOT, "build", "dual_issue_%s.hip" % TAG)
+BIN = os.path.join(ROOT, "build", "dual_issue_%s" % TAG)
 
 CLASSES = {
     "X": lambda d, a, b: f"v_xor_b32 v{d}, v{a}, v{b}",
@@ -32,7 +34,7 @@ CLASSES = {
     "B": lambda d, a, b: f"v_bitop3_b32 v{d}, v{a}, v{b}, v{(b + 2) % 24 + 24} bitop3:0x96",
     "N": None,  # no VALU: the other half alone
 }
-PAIRS = ["XX", "AA", "DD", "LL", "XA", "XD", "AD", "LA", "LD", "MA", "MD", "PA", "PD", "EA", "ED", "BA", "BD",
+PAIRS = os.environ.get("DUAL_PAIRS", "").split(",") if os.environ.get("DUAL_PAIRS") else ["XX", "AA", "DD", "LL", "XA", "XD", "AD", "LA", "LD", "MA", "MD", "PA", "PD", "EA", "ED", "BA", "BD",
          "XN", "AN", "DN", "AX", "DX"]
 # SPLIT: which waves run class A.  "half": waves 0-7 of a workgroup (older) vs 8-15; "alt": waves whose
 # index has bit 2 clear vs set -- every SIMD (wave w -> SIMD w % 4) then holds both classes in
