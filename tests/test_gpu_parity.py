@@ -4,7 +4,7 @@ Bit-exact throughout (integer work).  Run on an MI355X: ``pytest -m gpu``.
 Covers: every golden (root, nonce, value) triple through all three GPU hash paths
 (npow_values = the stream the search and sweep kernels run, the seq stream, the generic
 per-lane-root kernel); contiguous value ranges incl. 2^32 and 2^64 carries and 2^20 / 2^24
-ranges; every exhaustive sweep
+ranges, and 2^28 consecutive values of the shipped stream for two roots; every exhaustive sweep
 fixture (8 roots x [0, 2^28), hashlib ranges, the range across 2^64 -> 0) and,
 at BASELINE config 3's full size, the 2^36 sweep; first-win search validity
 at the BASELINE thresholds; threshold edges; exhaustion, cancellation,
@@ -15,6 +15,7 @@ import random
 import threading
 import time
 
+import numpy as np
 import pytest
 
 import oracle
@@ -40,8 +41,8 @@ PATHS = pytest.mark.parametrize("path", [_lib.NPOW_PATH_SEARCH, _lib.NPOW_PATH_S
 def test_golden_triples(gpu_engine, path):
     """Every golden (root, nonce, value) triple (hashlib) through one hash path, one root at a time:
     NPOW_PATH_SEARCH is the instruction stream the search and sweep kernels execute
-    (npow_values_kernel_ls2 -- the same uniform loads, priority runs and two workgroups per
-    CU), so its full 64-bit values are compared, not only its hit decisions."""
+    (npow_values_kernel_ls2 -- the same uniform loads, priority runs and four 512-lane
+    workgroups per CU), so its full 64-bit values are compared, not only its hit decisions."""
     g = load_golden("work_values.json")["triples"]
     got = [gpu_engine.values(bytes.fromhex(r), int(n, 16), 1, path=path)[0] for r, n, _ in g]
     assert [f"{v:016x}" for v in got] == [v for _, _, v in g]
@@ -79,6 +80,21 @@ def test_value_range_2p24_both_streams(gpu_engine):
     want = oracle.work_values_range(root, start, 1 << 24)
     assert (a == want).all() and (b == want).all()
     assert int(a[1 << 23]) == 0xfffffff4000d3dac  # the Nano genesis work
+
+
+def test_value_range_2p28_shipped_stream(gpu_engine):
+    """2^28 consecutive full 64-bit values of the stream the search and sweep kernels execute, every
+    one equal to the oracle's: 16 launches of 2^24 across the 2^40 carry of the nonce (bit 40 set
+    mid-range), for two roots.  The oracle side runs on the box's CPUs (~3 s per root)."""
+    for root_hex, start in (("7A0C6E2F1B3D5948E6A1C2B3D4E5F60718293A4B5C6D7E8F90A1B2C3D4E5F607", (1 << 40) - (1 << 27)),
+                            ("E89208DD038FBB269987689621D52292AE9C35941A7484756ECCED92A65093BA", 0x62f05417dd3fb691)):
+        root = bytes.fromhex(root_hex)
+        for k in range(16):
+            s = (start + (k << 24)) & ((1 << 64) - 1)
+            got = gpu_engine.values_array(root, s, 1 << 24, path=_lib.NPOW_PATH_SEARCH)
+            want = oracle.work_values_range(root, s, 1 << 24)
+            bad = np.flatnonzero(got != want)
+            assert bad.size == 0, f"root {root_hex[:8]}: {bad.size} values differ from {s + int(bad[0]):#x} on"
 
 
 def test_sweep_fixtures(gpu_engine):
