@@ -9,7 +9,7 @@ client/README.md:31):
                                 (nonces per launch in the reference, default 1048576) is a lower
                                 bound on a search launch's nonces (see apply_threads)
   -c/--cpu-threads N            rejected: this engine runs on MI355X GPUs only
-  --gpu-local-work-size N       accepted and ignored (workgroups are 256 lanes on gfx950)
+  --gpu-local-work-size N       accepted and ignored (search workgroups are 512 lanes on gfx950)
   --shuffle                     pick a random queued request instead of the oldest
   --max-active N                requests searched at once by the GPU work pool (default 4)
 
