@@ -296,6 +296,42 @@ BARRIER_LINES = ["s_barrier"]  # --sched lockstep: what ends an interval (+ "s_n
 # add included) after all its alignbits; "ad" also puts an s_barrier between the two runs; "fh" an
 # s_barrier between the full-rate and the half-rate part; "all" both barriers
 SPLIT = "none"
+# --run-order (round 3 power experiments): the order of the ops inside each run of a lockstep interval --
+# "id" (program order), "rev" (reverse), "shufN" (seeded shuffle); dependencies inside a run still hold
+RUN_ORDER = "id"
+
+
+def order_runs(units, ops_by_id):
+    """Reorder the units of each (interval, part) run per RUN_ORDER, topologically (Kahn)."""
+    if RUN_ORDER == "id":
+        return units
+    import heapq
+    import random
+    rng = random.Random(int(RUN_ORDER[4:]) if RUN_ORDER.startswith("shuf") else 0)
+    out, i = [], 0
+    while i < len(units):
+        j = i
+        while j < len(units) and units[j][1] == units[i][1]:
+            j += 1
+        grp = units[i:j]
+        ids = {u[0][0] for u in grp}
+        rank = {u[0][0]: (-u[0][0] if RUN_ORDER == "rev" else rng.random()) for u in grp}
+        deps = {u[0][0]: {p.id for p in ops_by_id[u[0][0]].preds if p.id in ids} for u in grp}
+        by_id = {u[0][0]: u for u in grp}
+        indeg = {k: len(v) for k, v in deps.items()}
+        users = {k: [m for m in ids if k in deps[m]] for k in ids}
+        heap = [(rank[k], k) for k in ids if indeg[k] == 0]
+        heapq.heapify(heap)
+        while heap:
+            _, k = heapq.heappop(heap)
+            out.append(by_id[k])
+            for m in users[k]:
+                indeg[m] -= 1
+                if indeg[m] == 0:
+                    heapq.heappush(heap, (rank[m], m))
+        assert len(out) == j, "cycle inside a run"
+        i = j
+    return out
 
 
 def op_cost(op: Op) -> float:
@@ -402,6 +438,7 @@ def schedule_lockstep(ops: List[Op], shift: bool = False, pad_end: bool = False)
         key = {k: (iv + ph, 1 - ph) for k, (iv, ph) in key.items()}
     units = sorted(key.items(), key=lambda kv: (kv[1][0], kv[1][1], kv[0][0]))
     idx = {op.id: op for op in ops}
+    units = order_runs(units, idx)
     items: list = []
     cur = None
     cur_ph = 0
@@ -1339,6 +1376,8 @@ def main() -> int:
     ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
     ap.add_argument("--fuse-out", choices=["bitop3", "none"], default="bitop3",
                     help="fold the output xors H0 ^ (v0 ^ v8) into v_bitop3_b32 (fuse_output_xor)")
+    ap.add_argument("--run-order", default="id",
+                    help="lockstep: op order inside each run -- id, rev, or shufN (seeded); experiments")
     ap.add_argument("--prio", choices=["none", "h", "a", "ad", "d"], default="none",
                     help="s_setprio at instruction-class changes (round 3 experiments, insert_setprio)")
     ap.add_argument("--pad", choices=["odd", "even", "none", "odd64", "even64", "odd128", "even128"], default="odd",
@@ -1371,8 +1410,9 @@ def main() -> int:
         lines, vmax, counts = allocate_and_emit(order_i, vrs, args.base, args.limit, VOP3_SIMPLE)
     else:
         if args.sched == "lockstep":
-            global ZPAIRS, BARRIER_LINES, SPLIT
+            global ZPAIRS, BARRIER_LINES, SPLIT, RUN_ORDER
             SPLIT = args.split
+            RUN_ORDER = args.run_order
             ZPAIRS = 6
             BARRIER_LINES = ["s_barrier", "s_nop 0"] if args.barrier_nop else ["s_barrier"]
             for op in reversed(ops):  # priorities are unused, but keep op.prio defined
@@ -1436,6 +1476,7 @@ def main() -> int:
               + (f" --func {args.func}" if args.func != "npow_asm_work_value" else "")
               + (f" --uload {args.uload}" if args.uload >= 0 else "")
               + (f" --split {args.split}" if args.split != "none" else "")
+              + (f" --run-order {args.run_order}" if args.run_order != "id" else "")
               + (f" --barrier-every {args.barrier_every}" if args.barrier_every != 1 else "")
               + (f" --base {args.base}" if args.base != 16 else "")
               + (f" --limit {args.limit}" if args.limit != 64 else "")
