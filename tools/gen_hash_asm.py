@@ -457,23 +457,40 @@ def schedule_lockstep(ops: List[Op], shift: bool = False, pad_end: bool = False)
 
 # ---------------------------------------------------------------------------------------
 # Register allocation + emission
+# --alloc (round 3 power experiments): which free VGPR the allocator takes -- the lowest (low), the
+# highest (high), or the next one after the last taken, wrapping (rr)
+ALLOC = "low"
+
+
 class Alloc:
     def __init__(self, base: int, limit: int) -> None:
         self.base, self.limit = base, limit
         self.free = set(range(base, limit))
         self.max_used = base
+        self.last = base - 1
+
+    def _order(self):
+        f = sorted(self.free)
+        if ALLOC == "high":
+            return f[::-1]
+        if ALLOC == "rr":
+            k = next((i for i, r in enumerate(f) if r > self.last), 0)
+            return f[k:] + f[:k]
+        return f
 
     def take1(self, avoid=()) -> int:
-        for r in sorted(self.free):
+        for r in self._order():
             if r not in avoid:
                 self.free.remove(r)
                 self.max_used = max(self.max_used, r + 1)
+                self.last = r
                 return r
         raise RuntimeError("out of VGPRs")
 
     def take2(self, avoid=()) -> int:
-        for r in sorted(self.free):
+        for r in self._order():
             if r % 2 == 0 and r + 1 in self.free and r not in avoid and r + 1 not in avoid:
+                self.last = r + 1
                 self.free.remove(r)
                 self.free.remove(r + 1)
                 self.max_used = max(self.max_used, r + 2)
@@ -1376,6 +1393,8 @@ def main() -> int:
     ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
     ap.add_argument("--fuse-out", choices=["bitop3", "none"], default="bitop3",
                     help="fold the output xors H0 ^ (v0 ^ v8) into v_bitop3_b32 (fuse_output_xor)")
+    ap.add_argument("--alloc", choices=["low", "high", "rr"], default="low",
+                    help="lockstep: VGPR allocation order (experiments)")
     ap.add_argument("--run-order", default="id",
                     help="lockstep: op order inside each run -- id, rev, or shufN (seeded); experiments")
     ap.add_argument("--prio", choices=["none", "h", "a", "ad", "d"], default="none",
@@ -1410,9 +1429,10 @@ def main() -> int:
         lines, vmax, counts = allocate_and_emit(order_i, vrs, args.base, args.limit, VOP3_SIMPLE)
     else:
         if args.sched == "lockstep":
-            global ZPAIRS, BARRIER_LINES, SPLIT, RUN_ORDER
+            global ZPAIRS, BARRIER_LINES, SPLIT, RUN_ORDER, ALLOC
             SPLIT = args.split
             RUN_ORDER = args.run_order
+            ALLOC = args.alloc
             ZPAIRS = 6
             BARRIER_LINES = ["s_barrier", "s_nop 0"] if args.barrier_nop else ["s_barrier"]
             for op in reversed(ops):  # priorities are unused, but keep op.prio defined
@@ -1477,6 +1497,7 @@ def main() -> int:
               + (f" --uload {args.uload}" if args.uload >= 0 else "")
               + (f" --split {args.split}" if args.split != "none" else "")
               + (f" --run-order {args.run_order}" if args.run_order != "id" else "")
+              + (f" --alloc {args.alloc}" if args.alloc != "low" else "")
               + (f" --barrier-every {args.barrier_every}" if args.barrier_every != 1 else "")
               + (f" --base {args.base}" if args.base != 16 else "")
               + (f" --limit {args.limit}" if args.limit != 64 else "")
