@@ -1100,7 +1100,7 @@ def _pair_regs(tok: str) -> List[str]:
 # insert_setprio raises a wave's priority while it runs half-rate instructions, so that a wave in its
 # full-rate run fills the shadows of another's alignbits instead of starving it.
 SETPRIO_MODES = {"h": {"A": 1, "D": 1, "F": 0}, "a": {"A": 1, "D": 0, "F": 0},
-                 "ad": {"A": 2, "D": 1, "F": 0}, "d": {"A": 0, "D": 1, "F": 0}}
+                 "ad": {"A": 2, "D": 1, "F": 0}, "d": {"A": 0, "D": 1, "F": 0}, "da": {"A": 1, "D": 2, "F": 0}}
 
 
 def insert_setprio(lines: List[str], mode: str) -> List[str]:
@@ -1397,7 +1397,7 @@ def main() -> int:
                     help="lockstep: VGPR allocation order (experiments)")
     ap.add_argument("--run-order", default="id",
                     help="lockstep: op order inside each run -- id, rev, or shufN (seeded); experiments")
-    ap.add_argument("--prio", choices=["none", "h", "a", "ad", "d"], default="none",
+    ap.add_argument("--prio", choices=["none", "h", "a", "ad", "d", "da"], default="none",
                     help="s_setprio at instruction-class changes (round 3 experiments, insert_setprio)")
     ap.add_argument("--pad", choices=["odd", "even", "none", "odd64", "even64", "odd128", "even128"], default="odd",
                     help="placement of the stream: 4 (mod 8) [odd], 0 (mod 8) [even], or as it falls; "
