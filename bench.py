@@ -469,6 +469,9 @@ class SclkSampler:
 
     def __init__(self, dev: int, period: float = 0.05):
         self.samples, self.bus, self.path = [], None, None
+        # the same card's hwmon power reading (microwatts) and its power cap, when readable: whether a
+        # run sits at the power limit that lowers its clock ("Priority runs")
+        self.power, self.pw_path, self.cap_w = [], None, None
         self.period, self._stop = period, threading.Event()
         try:
             hip = ctypes.CDLL("libamdhip64.so.7")
@@ -479,6 +482,18 @@ class SclkSampler:
                     if os.path.basename(os.path.realpath(d)).lower() == self.bus and \
                             os.path.exists(os.path.join(d, "pp_dpm_sclk")):
                         self.path = os.path.join(d, "pp_dpm_sclk")
+                        for h in sorted(glob.glob(os.path.join(d, "hwmon", "hwmon*"))):
+                            for name in ("power1_average", "power1_input"):
+                                if os.path.exists(os.path.join(h, name)):
+                                    self.pw_path = os.path.join(h, name)
+                                    break
+                            try:
+                                with open(os.path.join(h, "power1_cap")) as f:
+                                    self.cap_w = int(f.read()) / 1e6
+                            except (OSError, ValueError):
+                                pass
+                            if self.pw_path:
+                                break
                         break
         except (OSError, AttributeError):
             self.path = None
@@ -499,6 +514,12 @@ class SclkSampler:
                 return
             if v is not None:
                 self.samples.append(v)
+            if self.pw_path:
+                try:
+                    with open(self.pw_path) as f:
+                        self.power.append(int(f.read()) / 1e6)
+                except (OSError, ValueError):
+                    self.pw_path = None
             self._stop.wait(self.period)
 
     def __enter__(self):
@@ -518,6 +539,14 @@ class SclkSampler:
                 "max": max(self.samples), "samples": len(self.samples),
                 "source": f"current level of pp_dpm_sclk of rank 0's GPU ({self.bus}), every "
                           f"{int(self.period * 1e3)} ms over the warmup and timed searches"}
+
+    def power_summary(self):
+        if not self.power:
+            return None
+        return {"mean": round(statistics.mean(self.power), 1), "max": round(max(self.power), 1),
+                "cap": self.cap_w, "samples": len(self.power),
+                "source": f"hwmon {os.path.basename(self.pw_path or '')} of rank 0's GPU ({self.bus}) in W, with its "
+                          "power1_cap, sampled with the clock (the sensor updates more slowly than the samples)"}
 
 
 def _pmc(names=PMC_POOL):
@@ -1465,6 +1494,9 @@ def main() -> int:
         clk = sclk.summary()
         if clk:
             line["sysfs_sclk_mhz"] = clk
+        pw = sclk.power_summary()
+        if pw:
+            line["sysfs_power_w"] = pw
         line["host_worker_cpu"] = {"max_core_share": round(max(g[1] for g in gathered), 4),
                                    "what": "CPU time of the GPU's pool worker thread / wall time over the timed "
                                            "searches (libnanopow stats host_cpu_ms / host_wall_ms), max over ranks"}
