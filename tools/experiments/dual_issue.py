@@ -27,6 +27,8 @@ CLASSES = {
     "X": lambda d, a, b: f"v_xor_b32 v{d}, v{a}, v{b}",
     "E": lambda d, a, b: f"v_xor_b32_e64 v{d}, v{a}, v{b}",
     "A": lambda d, a, b: f"v_alignbit_b32 v{d}, v{a}, v{b}, 24",
+    "Y": lambda d, a, b: f"v_alignbyte_b32 v{d}, v{a}, v{b}, 3",
+    "R": lambda d, a, b: f"v_perm_b32 v{d}, v{a}, v{b}, s8",
     "D": lambda d, a, b: f"v_lshl_add_u64 v[{d & ~1}:{(d & ~1) + 1}], v[{a & ~1}:{(a & ~1) + 1}], 0, v[{b & ~1}:{(b & ~1) + 1}]",
     "L": lambda d, a, b: f"v_lshrrev_b32 v{d}, 31, v{a}",
     "M": lambda d, a, b: f"v_mov_b32 v{d}, v{a}",

@@ -261,7 +261,8 @@ def lower(dag: Dag, out: Node):
 
 
 # issue cost (SIMD cycles per wave64 instruction, profiles/r01_valu_ubench.json) and latency model
-COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b32": 4.3, "v_lshl_add_u64": 4.4,
+COST = {"v_xor_b32": 2.5, "v_xor_b32_s": 4.7, "v_xor_b32_k": 2.9, "v_alignbit_b32": 4.3, "v_alignbyte_b32": 4.3,
+        "v_lshl_add_u64": 4.4,
         "v_lshrrev_b32": 2.5, "v_mov_b32": 2.4, "v_add_co_u32": 2.1, "v_addc_co_u32": 2.1, "v_mad_u32_u24": 4.0,
         "v_bitop3_b32": 2.5}
 # 64-bit add as v_add_co_u32 + v_addc_co_u32 (carry through VCC) instead of one v_lshl_add_u64:
@@ -296,6 +297,7 @@ BARRIER_LINES = ["s_barrier"]  # --sched lockstep: what ends an interval (+ "s_n
 # add included) after all its alignbits; "ad" also puts an s_barrier between the two runs; "fh" an
 # s_barrier between the full-rate and the half-rate part; "all" both barriers
 SPLIT = "none"
+ROT_BYTE = False  # --rotbyte (round 3 power experiments): rotr24 / rotr16 halves as v_alignbyte_b32
 # --run-order (round 3 power experiments): the order of the ops inside each run of a lockstep interval --
 # "id" (program order), "rev" (reverse), "shufN" (seeded shuffle); dependencies inside a run still hold
 RUN_ORDER = "id"
@@ -730,6 +732,9 @@ def emit(order: List[Op], frontier: List[Node], out: Node, base: int, limit: int
                     lines.append(f"v_mad_u32_u24 v{r + h}, v{xb}, %[k{32 - n}], v{r + h}")
                     cnt("v_lshrrev_b32")
                     cnt("v_mad_u32_u24")
+                elif n < 32 and ROT_BYTE:  # --rotbyte: the byte-granular funnel shift (same class)
+                    lines.append(f"v_alignbyte_b32 v{r + h}, v{xb}, v{xa}, {n // 8}")
+                    cnt("v_alignbyte_b32")
                 elif n < 32:
                     lines.append(f"v_alignbit_b32 v{r + h}, v{xb}, v{xa}, {n}")
                     cnt("v_alignbit_b32")
@@ -1109,7 +1114,7 @@ def insert_setprio(lines: List[str], mode: str) -> List[str]:
     for ln in lines:
         opc = ln.split(" ", 1)[0]
         if opc.startswith("v_"):
-            cls = "A" if opc.startswith("v_alignbit") else ("D" if opc.startswith(("v_lshl_add_u64", "v_bitop3"))
+            cls = "A" if opc.startswith(("v_alignbit", "v_alignbyte")) else ("D" if opc.startswith(("v_lshl_add_u64", "v_bitop3"))
                                                             else "F")
             want = pr[cls]
             if want != cur:
@@ -1185,6 +1190,9 @@ def interpret(lines: List[str], nonce: int, uni_vals: List[int]) -> int:
         elif opc == "v_alignbit_b32":
             hi, lo, sh = rd32(ops[1]), rd32(ops[2]), int(ops[3])
             wr32(ops[0], (((hi << 32) | lo) >> sh) & M32)
+        elif opc == "v_alignbyte_b32":
+            hi, lo, sh = rd32(ops[1]), rd32(ops[2]), int(ops[3])
+            wr32(ops[0], (((hi << 32) | lo) >> (8 * (sh & 3))) & M32)
         elif opc == "v_lshrrev_b32":
             wr32(ops[0], rd32(ops[2]) >> int(ops[1]))
         elif opc == "v_mov_b32":
@@ -1393,6 +1401,8 @@ def main() -> int:
     ap.add_argument("--swapmov", action="store_true", help="rotr32 via in-place xors + v_mov_b32 swap")
     ap.add_argument("--fuse-out", choices=["bitop3", "none"], default="bitop3",
                     help="fold the output xors H0 ^ (v0 ^ v8) into v_bitop3_b32 (fuse_output_xor)")
+    ap.add_argument("--rotbyte", action="store_true",
+                    help="lockstep: rotr24 / rotr16 halves as v_alignbyte_b32 (experiments)")
     ap.add_argument("--alloc", choices=["low", "high", "rr"], default="low",
                     help="lockstep: VGPR allocation order (experiments)")
     ap.add_argument("--run-order", default="id",
@@ -1429,7 +1439,8 @@ def main() -> int:
         lines, vmax, counts = allocate_and_emit(order_i, vrs, args.base, args.limit, VOP3_SIMPLE)
     else:
         if args.sched == "lockstep":
-            global ZPAIRS, BARRIER_LINES, SPLIT, RUN_ORDER, ALLOC
+            global ZPAIRS, BARRIER_LINES, SPLIT, RUN_ORDER, ALLOC, ROT_BYTE
+            ROT_BYTE = args.rotbyte
             SPLIT = args.split
             RUN_ORDER = args.run_order
             ALLOC = args.alloc
@@ -1498,6 +1509,7 @@ def main() -> int:
               + (f" --split {args.split}" if args.split != "none" else "")
               + (f" --run-order {args.run_order}" if args.run_order != "id" else "")
               + (f" --alloc {args.alloc}" if args.alloc != "low" else "")
+              + (" --rotbyte" if args.rotbyte else "")
               + (f" --barrier-every {args.barrier_every}" if args.barrier_every != 1 else "")
               + (f" --base {args.base}" if args.base != 16 else "")
               + (f" --limit {args.limit}" if args.limit != 64 else "")
