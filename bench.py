@@ -149,6 +149,48 @@ def issue_bound_cycles(mix):
 PMC_POOL = ("r03s_pmc_pool.json", "r03w_pmc_pool.json", "r03p_pmc_pool.json", "r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
 PMC_SWEEP = ("r03s_pmc_sweep.json", "r03w_pmc_sweep.json", "r03p_pmc_sweep.json", "r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
 METRIC = "Gnonce/s blake2b-64 per GPU & 8-GPU node; p50 time-to-work at fffffff8"
+CSRC = os.path.join(HERE, "nano-dpow_amd", "csrc")
+
+
+def build_sha16() -> str:
+    """Identity of the libnanopow build: sha256 over the library's sources (kernel, generated streams,
+    host engine, C ABI header, Makefile), file names included.  The same sources rebuild the same
+    library, so a profile made from a bench line with this id describes this build."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(CSRC, "*.hip")) + glob.glob(os.path.join(CSRC, "*.cpp")) +
+                   glob.glob(os.path.join(CSRC, "*.h")) + glob.glob(os.path.join(CSRC, "*.inc")) +
+                   [os.path.join(CSRC, "Makefile"), os.path.join(HERE, "include", "nanopow.h")])
+    for f in files:
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def timed_region_profile(build: str):
+    """The committed rocprofv3 timed-region summary (tools/rocprof_timed_region.py) for this build: the
+    newest profiles/*_rocprofv3_timed_region.txt whose build_sha16 line equals `build`, else the newest one
+    at all (matches_this_build false).  Its fields as a dict, or None when there is none."""
+    import re
+    files = sorted(glob.glob(os.path.join(HERE, "profiles", "*_rocprofv3_timed_region.txt")), key=os.path.getmtime,
+                   reverse=True)
+    parsed = []
+    for f in files:
+        txt = open(f).read()
+        m = re.search(r"^build_sha16 ([0-9a-f]{16})", txt, re.M)
+        avg = re.search(r"timed region = the last (\d+) dispatches.*?average ([0-9.]+) ms", txt)
+        npl = re.search(r"^nonces_per_launch ([0-9]+)", txt, re.M)
+        fr = re.search(r"^frac_executed_from_profile ([0-9.]+)", txt, re.M)
+        if not (m and avg and npl):
+            continue
+        parsed.append({"file": "profiles/" + os.path.basename(f), "build_sha16": m.group(1),
+                       "matches_this_build": m.group(1) == build, "timed_dispatches": int(avg.group(1)),
+                       "avg_dispatch_ms": float(avg.group(2)), "nonces_per_launch": int(npl.group(1)),
+                       "frac_from_profile": float(fr.group(1)) if fr else None})
+    for p in parsed:
+        if p["matches_this_build"]:
+            return p
+    return parsed[0] if parsed else None
 
 
 def bench_root(i: int) -> bytes:
@@ -467,8 +509,8 @@ class SclkSampler:
     the card is found by the PCI bus id the HIP runtime reports.  Reading sysfs touches no GPU
     queue.  summary() is None when the file is unavailable."""
 
-    def __init__(self, dev: int, period: float = 0.05):
-        self.samples, self.bus, self.path = [], None, None
+    def __init__(self, dev: int, period: float = 0.05, span: str = "over the warmup and timed searches"):
+        self.samples, self.bus, self.path, self.span = [], None, None, span
         # the same card's hwmon power reading (microwatts) and its power cap, when readable: whether a
         # run sits at the power limit that lowers its clock (DESIGN.md section 4, "Priority runs")
         self.power, self.pw_path, self.cap_w = [], None, None
@@ -538,7 +580,7 @@ class SclkSampler:
         return {"mean": round(statistics.mean(self.samples), 1), "min": min(self.samples),
                 "max": max(self.samples), "samples": len(self.samples),
                 "source": f"current level of pp_dpm_sclk of rank 0's GPU ({self.bus}), every "
-                          f"{int(self.period * 1e3)} ms over the warmup and timed searches"}
+                          f"{int(self.period * 1e3)} ms {self.span}"}
 
     def power_summary(self):
         if not self.power:
@@ -584,9 +626,15 @@ LOOP_VALU = 5  # the search loop's VALU instructions per iteration besides the s
 def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, kern_nonces, launches, parallelism=None):
     gnps = tot_nonces / max_wall / 1e9
     per_rank_kernel_s = kern_ms * 1e-3 / world
-    achieved = (kern_nonces / world) * OPS_PER_NONCE / per_rank_kernel_s / 1e12 if kern_ms > 0 else 0.0
     mix = stream_mix()
     ex = mix["executed_int32_ops"]
+    # achieved / frac: the int32 ops the shipped stream executes per nonce (its header's mix); the
+    # algorithmic 2,232 of SURVEY.md §8(d) in achieved_algorithmic / frac_algorithmic -- the stream does
+    # less than that (host precompute, round 12's dead half), so only the executed count bounds frac by 1
+    achieved_alg = (kern_nonces / world) * OPS_PER_NONCE / per_rank_kernel_s / 1e12 if kern_ms > 0 else 0.0
+    achieved = achieved_alg * ex / OPS_PER_NONCE
+    build = build_sha16()
+    prof = timed_region_profile(build)
     pmc_name, pmc = _pmc(PMC_POOL)
     pmc_npd = pmc_nonces_per_dispatch(pmc, mix["valu"] + LOOP_VALU)
     return {
@@ -620,6 +668,7 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
         "mean_ttw_ms": round(statistics.mean(all_ttw) * 1e3, 3),
         "n_ttw": len(all_ttw),
         "gnps_per_gpu": round(gnps / world, 4),
+        "build_sha16": build,
         "roofline": {
             "bound": "valu",
             "kernel": STREAM["kernel"],
@@ -627,11 +676,21 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
             "peak": round(PEAK_TOPS, 3),
             "unit": "Tops/s (int32 VALU)",
             "frac": round(achieved / PEAK_TOPS, 4),
+            "achieved_what": f"kernel-hashed nonces x {ex} int32 ops the shipped stream executes per nonce "
+                             f"(executed_mix) / HIP-event-timed kernel time",
+            "achieved_algorithmic": round(achieved_alg, 3),
+            "frac_algorithmic": round(achieved_alg / PEAK_TOPS, 4),
+            "algorithmic_note": f"the same nonces x {OPS_PER_NONCE} algorithmic ops per nonce (SURVEY.md §8d): the "
+                                "stream executes fewer (round 1's three nonce-independent column steps on the host, "
+                                "round 12's dead half removed), so this fraction can pass 1",
             "peak_note": "peak = 256 CUs x 4 SIMDs x 32 lanes x 2.4 GHz, one wave64 VALU instruction per 2 cycles "
                          "per SIMD (MI355X_MICROARCH.md).  gfx950 also issues a full-rate instruction of one wave "
                          "in the shadow of another wave's v_alignbit_b32 (tools/experiments/dual_issue.py; PMC "
-                         "SQ_ACTIVE_INST_VALU2), which the stream's priority runs exploit, so frac can pass 1: "
-                         "issue_model holds the bound that applies to this instruction mix",
+                         "SQ_ACTIVE_INST_VALU2), which the stream's priority runs exploit; the GPU's power cap "
+                         "holds its clock below 2.4 GHz meanwhile (sclk_mhz): issue_model holds the bound that "
+                         "applies to this instruction mix",
+            "profile": (dict(prof, recompute=f"frac = nonces_per_launch x {ex} / avg_dispatch_ms / {PEAK_TOPS:.3f} Tops/s")
+                        if prof else None),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
             "traffic_unit": "HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
                             f"(profiles/{pmc_name}, tools/pmc_bench.sh); algorithmic bytes: 0",
@@ -640,7 +699,6 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
                         "fewer: host precompute of nonce-independent steps and round 12's dead half removed",
             "executed_ops_per_nonce": ex,
             "executed_mix": mix["mix"],
-            "frac_executed": round(achieved * ex / OPS_PER_NONCE / PEAK_TOPS, 4),
             "kernel_gnps": round(kern_nonces / (kern_ms * 1e-3) / 1e9, 4) if kern_ms > 0 else None,
             "avg_launch_ms": round(kern_ms / launches, 4) if launches else None,
             "nonces_per_launch": round(kern_nonces / launches) if launches else None,
@@ -1345,6 +1403,8 @@ def add_clock(line, clocks, over):
                         "source": "in-kernel: s_memtime / s_memrealtime spans of one wave per XCD in every "
                                   f"timed search launch (libnanopow stats clock_mhz), mean over {over}"}
     line["roofline"]["frac_at_measured_sclk"] = round(line["roofline"]["achieved"] / (256 * 128 * mhz * 1e6 / 1e12), 4)
+    line["roofline"]["frac_algorithmic_at_measured_sclk"] = round(
+        line["roofline"]["achieved_algorithmic"] / (256 * 128 * mhz * 1e6 / 1e12), 4)
     kg = line["roofline"]["kernel_gnps"]
     if kg:  # SIMD cycles per 64-nonce wave-hash at the in-kernel clock (1,024 SIMDs per GPU)
         n = line["n_gpus"]
@@ -1483,7 +1543,18 @@ def main() -> int:
     else:
         gathered = [local]
     kern_rate = res[4] / (res[3] * 1e-3) / 1e9 if res[3] > 0 else None
-    lat = latency_sample(eng, dev, args.latency_searches, kern_rate) if (WORLD == 1 and args.latency_searches) else None
+    lat, lat_clk = None, None
+    if WORLD == 1 and args.latency_searches:
+        # the card's clock and power over the ~11-s time-to-work leg too (the timed region is ~0.2 s at the
+        # driver's 20 steps: a handful of samples), every 25 ms, with the in-kernel clock of the same launches
+        eng.reset_stats(dev)
+        with SclkSampler(dev, period=0.025, span="over the time-to-work leg") as lat_sclk:
+            lat = latency_sample(eng, dev, args.latency_searches, kern_rate)
+        lat_clk = {"sysfs_sclk_mhz": lat_sclk.summary(), "sysfs_power_w": lat_sclk.power_summary(),
+                   "in_kernel_mhz": round(eng.stats(dev).clock_mhz, 1),
+                   "what": f"the {args.latency_searches} time-to-work searches (ttw_c_abi_ms; ~11 s of launches at "
+                           "fffffff8 and the receive-difficulty overhead sample) sampled every 25 ms; the in-kernel "
+                           "clock of their launches beside"}
     http = _http_ttw(eng, args.http_requests) if (rank == 0 and WORLD == 1 and args.http_requests) else None
     node = None
     if dist is not None and args.node_searches > 0 and int(os.environ.get("LOCAL_WORLD_SIZE", WORLD)) == WORLD:
@@ -1502,6 +1573,8 @@ def main() -> int:
                                            "searches (libnanopow stats host_cpu_ms / host_wall_ms), max over ranks"}
         if lat:
             line["ttw_c_abi_ms"] = lat
+        if lat_clk:
+            line["ttw_leg_clock_power"] = lat_clk
         if node:
             line["node_ttw_ms"] = node
         if http:

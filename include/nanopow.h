@@ -53,8 +53,11 @@ extern "C" {
 
 /* ABI revision (npow_abi_version()).  3: npow_values runs the search kernels' stream;
  * npow_values_path, npow_wait_info, npow_device_stats_get_sized added;
- * npow_device_stats_get writes only the revision-2 prefix of npow_device_stats. */
-#define NPOW_ABI_VERSION 3
+ * npow_device_stats_get writes only the revision-2 prefix of npow_device_stats.
+ * 4: npow_config_cpu_threads (CPU workers, --cpu-threads); npow_device_stats gains late_nonces,
+ * hip_device, cu_first; npow_search_info gains late_nonces_losers / late_nonces_winner (both structs
+ * are written up to the size the caller passes, so revision-3 callers are unaffected). */
+#define NPOW_ABI_VERSION 4
 
 /* Hash paths of npow_values_path. */
 #define NPOW_PATH_SEARCH 0  /* the instruction stream the search and sweep kernels execute
@@ -92,6 +95,13 @@ typedef struct npow_device_stats {
   /* ---- ABI 3 (npow_device_stats_get_sized only) ---- */
   uint64_t kills_relayed;   /* losing jobs of this device stopped by another device's win: the deciding
                                thread raised this device's kill word directly (no wait for its worker) */
+  /* ---- ABI 4 ---- */
+  uint64_t late_nonces;     /* device-side overshoot of the search kernels: nonces hashed by workgroups in
+                               iterations that started after one of their waves knew the job was over (its
+                               dead word, a win, a kill read by a poll) -- counted in the kernel */
+  int32_t hip_device;       /* HIP device this logical device runs on (-1: the CPU workers) */
+  int32_t cu_first;         /* -1: the whole GPU; else the first CU of its partition (NANOPOW_VIRTUAL_DEVICES:
+                               a CU-masked stream over CUs [cu_first, cu_first + cus)) */
 } npow_device_stats;
 
 /* Outcome of one search (npow_wait_info).  Times are host steady-clock microseconds since
@@ -112,7 +122,22 @@ typedef struct npow_search_info {
   double finish_us;         /* every device done with the job */
   double stop_after_decide_us;
   uint64_t overshoot_nonces;
+  /* ---- ABI 4: counted on the devices (npow_device_stats.late_nonces, per job) ---- */
+  uint64_t late_nonces_losers;  /* nonces the other devices' waves hashed for the job after they knew it was
+                                   over (the kill relayed into their dead word); the host-side bound above
+                                   adds the kill's way there and the worker's observation */
+  uint64_t late_nonces_winner;  /* the same on the deciding device after its own win */
 } npow_search_info;
+
+/* CPU workers (nano-work-server.exe @1681064 `--cpu-threads N`): before npow_init, ask it to add
+ * `threads` host threads (0 = none, the default; at most 1024) as one more logical device after the
+ * GPUs.  Searches whose device_mask selects it (mask 0 = all devices does) give it a stride of
+ * their own like a GPU; its threads hash with the library's own CPU work value (the function that
+ * re-validates GPU winners), one job at a time, and the first valid result from any device decides
+ * the job.  Sweeps and values run on GPUs only.  npow_init still fails without a GPU: the CPU workers
+ * run beside GPUs, never instead of them.  Its npow_device_stats has hip_device = -1, cus = threads.
+ * NPOW_ERR_BAD_ARGUMENT after npow_init. */
+int npow_config_cpu_threads(uint32_t threads);
 
 /* Open every visible HIP device, create its stream and buffers.
  * Replaces the work server's OpenCL device set-up for `--gpu P:D[:THREADS]`

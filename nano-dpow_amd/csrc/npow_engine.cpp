@@ -76,6 +76,13 @@ std::vector<Device*> select_devices(uint64_t mask) {
   return out;
 }
 
+std::vector<Device*> select_gpus(uint64_t mask) {
+  std::vector<Device*> out;
+  for (Device* d : select_devices(mask))
+    if (!d->cpu_threads) out.push_back(d);
+  return out;
+}
+
 void account_launch(Device& d, int ring) {
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, d.ev_start[ring], d.ev_stop[ring]) != hipSuccess) ms = 0.f;
@@ -88,9 +95,11 @@ namespace {
 
 std::mutex g_mu;
 bool g_init = false;
+uint32_t g_cpu_threads = 0;  // npow_config_cpu_threads: CPU workers npow_init adds as one more device
 
 constexpr uint64_t kHitCap = 1u << 20;        // per-device sweep hit buffer (8 MiB)
 constexpr uint64_t kValuesChunk = 1u << 24;   // values mode: nonces per launch (128 MiB out)
+constexpr uint64_t kPairsChunk = 1u << 22;    // npow_values_pairs: pairs per launch (168 MiB of host staging)
 
 // One in-flight launch.
 struct Inflight {
@@ -176,6 +185,7 @@ int check_init() {
 
 // Release one device's resources (any of them may be missing: a partial npow_init).
 void free_device(Device& d) {
+  if (d.cpu_threads) return;  // no HIP state
   (void)hipSetDevice(d.hip_id);
   if (d.stream) (void)hipStreamSynchronize(d.stream);
   for (int r = 0; r < kEventRing; ++r) {
@@ -189,8 +199,14 @@ void free_device(Device& d) {
   if (d.stream) (void)hipStreamDestroy(d.stream);
 }
 
-// Create one device's stream, buffers and events (d is already in g_devs).
-int init_device(Device& d, int n_physical) {
+// Create one device's stream, buffers and events (d is already in g_devs).  parts > 1: logical device
+// d.id is partition d.id / n_physical of HIP device d.id % n_physical, a CU-masked stream
+// (hipExtStreamCreateWithCUMask) over CUs [part * cus / parts, (part + 1) * cus / parts) -- measured on the
+// MI355X (tools/experiments/cu_mask_probe.hip, profiles/r04_cu_mask_probe.txt): such a contiguous run of
+// mask bits holds the same number of CUs on each of the 8 XCDs, the partitions are disjoint, and kernels
+// on up to 8 of them run at the same time, each from its start; a mask of every parts-th CU is NOT a
+// partition (its workgroups ran on every CU).
+int init_device(Device& d, int n_physical, int parts) {
   d.hip_id = d.id % n_physical;
   HIPTRY(hipSetDevice(d.hip_id));
   const char* f = test_hooks_enabled() ? getenv("NANOPOW_FAULT_INIT") : nullptr;
@@ -202,7 +218,19 @@ int init_device(Device& d, int n_physical) {
   hipDeviceProp_t p;
   HIPTRY(hipGetDeviceProperties(&p, d.hip_id));
   d.cus = p.multiProcessorCount;
-  HIPTRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  if (parts > 1) {
+    const int part = d.id / n_physical, all = p.multiProcessorCount;
+    const int lo = part * all / parts, hi = (part + 1) * all / parts;
+    std::vector<uint32_t> mask((size_t)(all + 31) / 32, 0u);
+    for (int i = lo; i < hi; ++i) mask[(size_t)i / 32] |= 1u << (i % 32);
+    // the stream is a blocking one (no flags argument): every copy of this device goes on it, never on the
+    // null stream, which would wait for the other partitions' launches
+    HIPTRY(hipExtStreamCreateWithCUMask(&d.stream, (uint32_t)mask.size(), mask.data()));
+    d.cus = hi - lo;
+    d.cu_first = lo;
+  } else {
+    HIPTRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+  }
   HIPTRY(hipMalloc(&d.st, sizeof(DevState)));
   HIPTRY(hipMalloc(&d.d_out, kValuesChunk * sizeof(uint64_t)));
   void* mb = nullptr;
@@ -272,7 +300,8 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
   const uint64_t k = std::min<uint64_t>(hs.n_hits, kHitCap);
   hits.resize(k);
   if (k) {
-    HIPTRY(hipMemcpy(hits.data(), d.d_out, k * sizeof(uint64_t), hipMemcpyDeviceToHost));
+    HIPTRY(hipMemcpyAsync(hits.data(), d.d_out, k * sizeof(uint64_t), hipMemcpyDeviceToHost, d.stream));
+    HIPTRY(hipStreamSynchronize(d.stream));
   }
   return NPOW_OK;
 }
@@ -287,7 +316,7 @@ extern "C" {
 const char* npow_last_error(void) { return t_err.c_str(); }
 
 const char* npow_version(void) {
-  return "libnanopow 0.3 (ABI 3; gfx950 HIP kernels: blake2b-64 nonce search, four 512-lane workgroups per CU, priority runs; "
+  return "libnanopow 0.4 (ABI 4; gfx950 HIP kernels: blake2b-64 nonce search, four 512-lane workgroups per CU, priority runs; "
          "v_lshl_add_u64 adds, v_alignbit rotations)";
 }
 
@@ -311,18 +340,35 @@ int npow_init(int* n_devices) try {
   int n_logical = n;
   if (const char* v = getenv("NANOPOW_VIRTUAL_DEVICES")) {
     const int k = atoi(v);
-    if (k > 0) n_logical = k;
+    if (k > 0) n_logical = std::min(k, 64);
   }
-  for (int i = 0; i < n_logical && i < 64; ++i) {
+  // Logical devices beyond the physical ones split each GPU's CUs into disjoint partitions (round 4: a
+  // faithful stand-in for separate GPUs -- every device's launch runs from its start on CUs of its own),
+  // when they divide evenly, at most 8 per GPU; NANOPOW_VIRTUAL_PARTITION=share makes them time-share
+  // the whole GPU instead (rounds 1-3).
+  int parts = 1;
+  if (n_logical > n && n_logical % n == 0 && n_logical / n <= 8) {
+    const char* vp = getenv("NANOPOW_VIRTUAL_PARTITION");
+    if (!vp || strcmp(vp, "share") != 0) parts = n_logical / n;
+  }
+  for (int i = 0; i < n_logical; ++i) {
     g_devs.push_back(std::make_unique<Device>());
     g_devs.back()->id = i;
-    if (int rc = init_device(*g_devs.back(), n)) {
+    if (int rc = init_device(*g_devs.back(), n, parts)) {
       // leave nothing behind: a retried npow_init starts from an empty device list
       const std::string msg = last_error();
       for (auto& d : g_devs) free_device(*d);
       g_devs.clear();
       return fail(rc, msg);
     }
+  }
+  if (g_cpu_threads > 0 && g_devs.size() < 64) {  // the CPU workers: one more logical device, after the GPUs
+    g_devs.push_back(std::make_unique<Device>());
+    Device& c = *g_devs.back();
+    c.id = (int)g_devs.size() - 1;
+    c.cpu_threads = (int)g_cpu_threads;
+    c.cus = (int)g_cpu_threads;
+    c.hip_id = -1;
   }
   g_init = true;
   pool_start();
@@ -357,6 +403,14 @@ uint64_t npow_work_value(const uint8_t root[32], uint64_t nonce) {
   for (int i = 0; i < 4; ++i) m[i] = host_load_le64(root + 8 * i);
   return host_work_value(m, nonce);
 }
+
+int npow_config_cpu_threads(uint32_t threads) try {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_init) return fail(NPOW_ERR_BAD_ARGUMENT, "npow_config_cpu_threads must precede npow_init");
+  if (threads > 1024) return fail(NPOW_ERR_BAD_ARGUMENT, "threads must be <= 1024");
+  g_cpu_threads = threads;
+  return NPOW_OK;
+} catch (...) { return guard_exception(); }
 
 int npow_set_tuning(uint32_t iters_per_launch, uint32_t poll_interval, uint32_t blocks_per_cu) try {
   if (iters_per_launch) {
@@ -411,7 +465,7 @@ static int stats_fill(int device, npow_device_stats* out) {
   out->kernel_ms = d.kernel_ms;
   out->invalid_work = d.invalid;
   out->cus = d.cus;
-  out->grid = ls_grid(d);
+  out->grid = d.cpu_threads ? 0 : ls_grid(d);
   out->clock_mhz = d.clk_ref_ticks > 0 ? d.clk_ticks / d.clk_ref_ticks * 100.0 : 0.0;
   out->host_cpu_ms = cpu - d.worker_cpu0_ms;
   out->host_wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - d.stats_t0).count();
@@ -422,11 +476,15 @@ static int stats_fill(int device, npow_device_stats* out) {
   out->yields = d.yields;
   out->dyn_entries = d.dyn;
   out->kills_relayed = d.kills_relayed;
+  out->late_nonces = d.late;
+  out->hip_device = d.hip_id;
+  out->cu_first = d.cu_first;
   return NPOW_OK;
 }
 
 // ABI 2 callers allocate the struct up to dyn_entries: never write past it here.
 int npow_device_stats_get(int device, npow_device_stats* out) try {
+  if (!out) return fail(NPOW_ERR_BAD_ARGUMENT, "out is required");
   npow_device_stats full;
   if (int rc = stats_fill(device, &full)) return rc;
   memcpy(out, &full, offsetof(npow_device_stats, kills_relayed));
@@ -434,6 +492,7 @@ int npow_device_stats_get(int device, npow_device_stats* out) try {
 } catch (...) { return guard_exception(); }
 
 int npow_device_stats_get_sized(int device, npow_device_stats* out, uint64_t size) try {
+  if (!out || size == 0) return fail(NPOW_ERR_BAD_ARGUMENT, "out and size > 0 are required");
   npow_device_stats full;
   if (int rc = stats_fill(device, &full)) return rc;
   memcpy(out, &full, std::min<uint64_t>(size, sizeof(full)));
@@ -447,7 +506,7 @@ int npow_device_stats_reset(int device) try {
   settle_stats(d);
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
-  d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = d.kills_relayed = 0;
+  d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = d.kills_relayed = d.late = 0;
   d.kernel_ms = 0.0;
   d.clk_ticks = d.clk_ref_ticks = 0.0;
   d.stats_t0 = std::chrono::steady_clock::now();
@@ -557,8 +616,8 @@ int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint6
                const volatile uint32_t* cancel, uint64_t* out, uint64_t cap, uint64_t* n_out) try {
   if (int rc = check_init()) return rc;
   if (!root || !n_out || (cap && !out)) return fail(NPOW_ERR_BAD_ARGUMENT, "root, n_out (and out when cap>0) required");
-  auto devs = select_devices(device_mask);
-  if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable device in device_mask");
+  auto devs = select_gpus(device_mask);
+  if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable GPU in device_mask");
   const RootPrecomp pre = host_precompute(root);
   const size_t G = devs.size();
   std::vector<std::vector<uint64_t>> hits(G);
@@ -605,8 +664,8 @@ int npow_sweep(const uint8_t root[32], uint64_t threshold, uint64_t start, uint6
 static int values_on(int device, const uint8_t root[32], uint64_t start, uint64_t count, Mode mode,
                      uint64_t* values_out) {
   if (int rc = check_init()) return rc;
-  if (device < 0 || device >= (int)g_devs.size() || !root || (count && !values_out))
-    return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
+  if (device < 0 || device >= (int)g_devs.size() || !root || (count && !values_out) || g_devs[device]->cpu_threads)
+    return fail(NPOW_ERR_BAD_ARGUMENT, "bad device (or the CPU device) or null buffer");
   Device& d = *g_devs[device];
   TaskLock lk(d);
   HIPTRY(hipSetDevice(d.hip_id));
@@ -639,46 +698,58 @@ int npow_values_path(int device, const uint8_t root[32], uint64_t start, uint64_
   if (path == NPOW_PATH_SEQ) return values_on(device, root, start, count, Mode::kValuesSeq, values_out);
   if (path == NPOW_PATH_GENERIC) {
     if (count > 0xffffffffull) return fail(NPOW_ERR_BAD_ARGUMENT, "generic path: count must be < 2^32");
-    std::vector<uint8_t> roots((size_t)count * 32);
-    std::vector<uint64_t> nonces((size_t)count);
-    for (uint64_t i = 0; i < count; ++i) {
-      memcpy(&roots[(size_t)i * 32], root, 32);
-      nonces[(size_t)i] = start + i;
+    // in chunks of kPairsChunk pairs through one reused buffer (one call could otherwise
+    // need ~160 GiB of host memory for its per-pair roots)
+    const uint64_t chunk = std::min<uint64_t>(count, kPairsChunk);
+    std::vector<uint8_t> roots((size_t)chunk * 32);
+    std::vector<uint64_t> nonces((size_t)chunk);
+    for (uint64_t i = 0; i < chunk; ++i) memcpy(&roots[(size_t)i * 32], root, 32);
+    for (uint64_t off = 0; off < count; off += chunk) {
+      const uint64_t cnt = std::min(chunk, count - off);
+      for (uint64_t i = 0; i < cnt; ++i) nonces[(size_t)i] = start + off + i;
+      if (int rc = npow_values_pairs(device, roots.data(), nonces.data(), (uint32_t)cnt, values_out + off)) return rc;
     }
-    return npow_values_pairs(device, roots.data(), nonces.data(), (uint32_t)count, values_out);
+    return NPOW_OK;
   }
   return fail(NPOW_ERR_BAD_ARGUMENT, "path must be NPOW_PATH_SEARCH, NPOW_PATH_SEQ or NPOW_PATH_GENERIC");
 } catch (...) { return guard_exception(); }
 
 int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, uint32_t n, uint64_t* values_out) try {
   if (int rc = check_init()) return rc;
-  if (device < 0 || device >= (int)g_devs.size() || (n && (!roots || !nonces || !values_out)))
-    return fail(NPOW_ERR_BAD_ARGUMENT, "bad device or null buffer");
+  if (device < 0 || device >= (int)g_devs.size() || (n && (!roots || !nonces || !values_out)) ||
+      g_devs[device]->cpu_threads)
+    return fail(NPOW_ERR_BAD_ARGUMENT, "bad device (or the CPU device) or null buffer");
   if (n == 0) return NPOW_OK;
   Device& d = *g_devs[device];
   TaskLock lk(d);
   HIPTRY(hipSetDevice(d.hip_id));
-  std::vector<uint64_t> words((size_t)n * 4);
-  for (uint32_t i = 0; i < n; ++i)
-    for (int k = 0; k < 4; ++k) words[4 * (size_t)i + k] = host_load_le64(roots + 32 * (size_t)i + 8 * k);
+  // chunks of kPairsChunk pairs through device buffers allocated once per call; every copy on the
+  // device's own stream (a CU-partitioned logical device's stream is a blocking one, so the null
+  // stream would wait for the other partitions' launches)
+  const uint32_t chunk = (uint32_t)std::min<uint64_t>(n, kPairsChunk);
+  std::vector<uint64_t> words((size_t)chunk * 4);
   uint64_t *dw = nullptr, *dn = nullptr, *dv = nullptr;
-  HIPTRY(hipMalloc(&dw, words.size() * 8));
-  HIPTRY(hipMalloc(&dn, (size_t)n * 8));
-  HIPTRY(hipMalloc(&dv, (size_t)n * 8));
   int rc = NPOW_OK;
-  do {
-    hipError_t e;
-    if ((e = hipMemcpy(dw, words.data(), words.size() * 8, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = hipMemcpy(dn, nonces, (size_t)n * 8, hipMemcpyHostToDevice)) != hipSuccess ||
-        (e = launch_pairs((int)((n + kBlock - 1) / kBlock), d.stream, dw, dn, n, dv)) != hipSuccess ||
-        (e = hipStreamSynchronize(d.stream)) != hipSuccess ||
-        (e = hipMemcpy(values_out, dv, (size_t)n * 8, hipMemcpyDeviceToHost)) != hipSuccess) {
-      rc = fail(NPOW_ERR_HIP, std::string("values_pairs: ") + hipGetErrorString(e));
+  hipError_t e = hipSuccess;
+  if ((e = hipMalloc(&dw, words.size() * 8)) == hipSuccess && (e = hipMalloc(&dn, (size_t)chunk * 8)) == hipSuccess &&
+      (e = hipMalloc(&dv, (size_t)chunk * 8)) == hipSuccess) {
+    for (uint32_t off = 0; off < n && e == hipSuccess; off += std::min(chunk, n - off)) {
+      const uint32_t cnt = std::min(chunk, n - off);
+      for (uint32_t i = 0; i < cnt; ++i)
+        for (int k = 0; k < 4; ++k)
+          words[4 * (size_t)i + k] = host_load_le64(roots + 32 * ((size_t)off + i) + 8 * k);
+      if ((e = hipMemcpyAsync(dw, words.data(), (size_t)cnt * 32, hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
+          (e = hipMemcpyAsync(dn, nonces + off, (size_t)cnt * 8, hipMemcpyHostToDevice, d.stream)) != hipSuccess ||
+          (e = launch_pairs((int)((cnt + kBlock - 1) / kBlock), d.stream, dw, dn, cnt, dv)) != hipSuccess ||
+          (e = hipMemcpyAsync(values_out + off, dv, (size_t)cnt * 8, hipMemcpyDeviceToHost, d.stream)) != hipSuccess ||
+          (e = hipStreamSynchronize(d.stream)) != hipSuccess)
+        break;
     }
-  } while (0);
-  (void)hipFree(dw);
-  (void)hipFree(dn);
-  (void)hipFree(dv);
+  }
+  if (e != hipSuccess) rc = fail(NPOW_ERR_HIP, std::string("values_pairs: ") + hipGetErrorString(e));
+  if (dw) (void)hipFree(dw);
+  if (dn) (void)hipFree(dn);
+  if (dv) (void)hipFree(dv);
   return rc;
 } catch (...) { return guard_exception(); }
 

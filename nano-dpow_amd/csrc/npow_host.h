@@ -33,8 +33,11 @@ static_assert(kEventRing == sizeof(PoolMailbox::clk) / sizeof(PoolMailbox::clk[0
 
 struct Device {
   int id = 0;       // logical index (device_mask bit)
+  int cpu_threads = 0;  // > 0: not a GPU but the pool's CPU workers (npow_cpu.cpp, --cpu-threads); no HIP state
   int hip_id = 0;   // HIP device (== id unless NANOPOW_VIRTUAL_DEVICES is set)
-  int cus = 0;
+  int cus = 0;       // CUs the device's kernels run on (its partition's, see cu_first)
+  int cu_first = -1; // -1: the whole GPU; else the first CU of this logical device's partition (a CU-masked
+                     // stream over [cu_first, cu_first + cus) of HIP device hip_id; npow_engine.cpp init_device)
   hipStream_t stream = nullptr;
   DevState* st = nullptr;        // device memory (sweep / values tasks)
   HostMailbox* mb = nullptr;     // pinned host (coherent), host view
@@ -59,6 +62,7 @@ struct Device {
   uint64_t early = 0, early_mismatch = 0;  // jobs finished from a published final count (npow_pool.cpp)
   uint64_t yields = 0, dyn = 0;            // launches yielded / jobs that joined a running launch
   uint64_t kills_relayed = 0;              // losing jobs stopped by another device's decision (npow_pool.cpp)
+  uint64_t late = 0;                       // device-side overshoot: nonces hashed after the job was known over
   // Published by the pool worker for npow_device_stats_get: it has launches or slots in flight, and
   // how many of its slots are still searching.  A job finished early returns before the launch that
   // held it is retired; with no slot searching, the stats wait for the worker to retire the rest.
@@ -122,8 +126,10 @@ class TaskLock {
   std::unique_lock<std::mutex> lk_;
 };
 
-// Devices selected by a mask (0 = all), excluding dead ones.
+// Devices selected by a mask (0 = all), excluding dead ones; select_gpus also excludes the CPU device
+// (sweeps and values run on GPUs only).
 std::vector<Device*> select_devices(uint64_t mask);
+std::vector<Device*> select_gpus(uint64_t mask);
 // Per-launch event accounting (kernel time by HIP events on the launch's own stream).
 void account_launch(Device& d, int ring);
 

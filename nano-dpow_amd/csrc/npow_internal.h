@@ -159,10 +159,15 @@ struct PoolSlotCount {
   unsigned long long wgs;
   uint8_t pad[56];
 };
+// Word kLateWord of each done shard's line: the device-side overshoot -- nonces a workgroup hashed for the
+// entry in iterations that started after one of its waves knew the entry was over (its dead word, a win, or a
+// kill read by its poll), added when it leaves the entry.  Cumulative per slot like the done counts.
+constexpr int kLateWord = 1;
 struct PoolDevState {
   PoolSlotWord slot[kMaxSlots];
   PoolSlotCount count[kMaxSlots][kWgsShards];
-  unsigned long long done[kMaxSlots][kPoolDoneShards * 8];  // nonces hashed, sharded over 64-B lines
+  unsigned long long done[kMaxSlots][kPoolDoneShards * 8];  // nonces hashed (word 0) and late ones (word
+                                                            // kLateWord), sharded over 64-B lines
 };
 
 // Pinned host-coherent mailbox of the pool: one win record per slot (the winner stores
@@ -185,9 +190,10 @@ struct PoolClk {
 // no workgroup is left on it and none can join, so a won or killed job finishes without waiting
 // for its launch to end (the other entries may keep it running for the rest of its budget).
 struct alignas(64) PoolFin {
-  uint64_t gen;    // released after total
+  uint64_t gen;    // released after total and late
   uint64_t total;  // the slot's done shards, summed (cumulative over its generations)
-  uint8_t pad[48];
+  uint64_t late;   // the slot's late words, summed (kLateWord; cumulative)
+  uint8_t pad[40];
 };
 // An unbounded job adopted while a search launch runs joins that launch instead of ending it
 // (a yield): the host writes its entry at ring position p (dyn[p % kDynEntries]) and then releases

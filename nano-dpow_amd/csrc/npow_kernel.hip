@@ -243,7 +243,7 @@ __global__ __launch_bounds__(kLsBlock, 8) void npow_sweep_kernel_ls2(const Launc
 // ---- Values through the shipped stream (npow_values_kernel_ls2) ----------------------------------
 // Every value of [base, base + count), hashed by exactly the instruction stream the search and sweep
 // kernels run (npow_hash_asm_lockstep_ld.inc: the same uniform loads, the same priority runs, the
-// same two-workgroups-per-CU shape), so the parity tests compare that stream's 64-bit values with the
+// same shape of four 512-lane workgroups per CU), so the parity tests compare that stream's 64-bit values with the
 // oracle -- not only its hit / no-hit decisions.  Rows of kLsWaves blocks (one per wave) go to workgroups
 // round-robin; every wave of a workgroup runs the same number of rows (workgroup-uniform control
 // flow, as the search kernel's), and lanes past the range's end hash but do not store.
@@ -352,8 +352,8 @@ __device__ __forceinline__ void clk_end_ls2(const PoolTable* tab, PoolMailbox* m
 //  * a workgroup works on one entry at a time (its own entry g % n first; bounded entries are dense
 //    over their own workgroups' waves, PoolEntry comment with unit = workgroup);
 //  * a wave that wants its workgroup to stop (a win, a dead / killed / yielded entry, the time
-//    budget) files a request in LDS, s_stop[segment % 3] = min((it + 1) << 1 | kind) with kind 0 =
-//    end the launch, 1 = leave the entry, drained before the iteration's closing s_barrier; every
+//    budget) files a request in LDS, s_stop[segment % 3] = min((it + 1) << 2 | kind) with kind 0 =
+//    end the launch, 1-3 = leave the entry (why: see the loop), drained before the iteration's closing s_barrier; every
 //    wave reads the word at the top of an iteration, so all waves see the same set of requests and
 //    leave together, one hash after the request (~16 us);
 //  * leaving an entry: wave 0 picks the next entry and broadcasts it through LDS (one
@@ -399,11 +399,15 @@ __device__ __forceinline__ bool ls2_empty(PoolDevState* st, uint32_t slot) {
 __device__ __forceinline__ uint32_t ls2_shard() { return blockIdx.x % kWgsShards; }
 
 __device__ __forceinline__ void ls2_publish_fin(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen) {
-  unsigned long long total = 0;
-#pragma unroll 4
-  for (int i = 0; i < kPoolDoneShards; ++i)
+  unsigned long long total = 0, late = 0;
+#pragma unroll 1
+  for (int i = 0; i < kPoolDoneShards; ++i) {  // (unrolled, the two sums spilled to scratch: this is inlined into
+                                               // the poll branch of the search loop, where SGPRs are all taken)
     total += __hip_atomic_load(&st->done[slot][i * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    late += __hip_atomic_load(&st->done[slot][i * 8 + kLateWord], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   __hip_atomic_store(&mb->fin[slot].total, (uint64_t)total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&mb->fin[slot].late, (uint64_t)late, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&mb->fin[slot].gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -440,16 +444,19 @@ __device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint
 // done shards load in parallel (one lane per shard) instead of ~40 round trips one after another --
 // the last leaver's publish is on the path of a won job's reply.
 __device__ __forceinline__ void ls2_leave_wave(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
-                                               uint32_t sum, bool counted) {
+                                               uint32_t sum, uint32_t late, bool counted) {
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  unsigned long long* const shard = &st->done[slot][(blockIdx.x % kPoolDoneShards) * 8];
   unsigned long long old = 0;
   if (!counted) {
-    if (lane == 0 && sum) atomicAdd(&st->done[slot][(blockIdx.x % kPoolDoneShards) * 8], (unsigned long long)sum);
+    if (lane == 0 && sum) atomicAdd(shard, (unsigned long long)sum);
+    if (lane == 0 && late) atomicAdd(shard + kLateWord, (unsigned long long)late);
     return;
   }
   if (lane == 0) {
-    if (sum) atomicAdd(&st->done[slot][(blockIdx.x % kPoolDoneShards) * 8], (unsigned long long)sum);
-    ls2_complete();  // the count first
+    if (sum) atomicAdd(shard, (unsigned long long)sum);
+    if (late) atomicAdd(shard + kLateWord, (unsigned long long)late);
+    ls2_complete();  // the counts first
     old = __hip_atomic_fetch_add(&st->count[slot][ls2_shard()].wgs, ~0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     ls2_complete();
   }
@@ -462,13 +469,16 @@ __device__ __forceinline__ void ls2_leave_wave(PoolDevState* st, PoolMailbox* mb
                     __hip_atomic_load(&st->count[slot][lane].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   ls2_complete();
   if (__ballot(busy) != 0) return;
-  unsigned long long t = lane < kPoolDoneShards
-                             ? __hip_atomic_load(&st->done[slot][lane * 8], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                             : 0ull;
+  // lanes 0..31: the done shards, lanes 32..63: the late words of the same lines; summed per half
+  static_assert(kPoolDoneShards == 32, "one half-wave per counter");
+  unsigned long long t = __hip_atomic_load(&st->done[slot][(lane & 31) * 8 + (lane < 32 ? 0 : kLateWord)],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-  for (int m = 32; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+  for (int m = 16; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+  const unsigned long long t_late = readlane64(t, 32);
   if (lane == 0) {
     __hip_atomic_store(&mb->fin[slot].total, (uint64_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mb->fin[slot].late, (uint64_t)t_late, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&mb->fin[slot].gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -519,12 +529,12 @@ __device__ __forceinline__ unsigned long long ls2_wgs(PoolDevState* st, uint32_t
   return __hip_atomic_load(&st->count[slot][ls2_shard()].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// A polling wave (lane 0 only): the host words of the entry.  Returns true when the wave's
-// workgroup must leave the entry: new jobs wait and the entry is unbounded (a yield), it was
+// A polling wave (lane 0 only): the host words of the entry.  Returns bit 0 set when the wave's
+// workgroup must leave the entry, and bit 1 too when the reason is the pinned kill word: new jobs wait and the entry is unbounded (a yield), it was
 // killed, or it is unbounded and a dynamic entry has at least two workgroups fewer than it (the
 // workgroup moves there: a job that joined the running launch collects its share a workgroup at a
 // time, each from the most crowded entry among the pollers).
-__device__ __forceinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
+__device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
                                          uint32_t* seen) {
   const ConstEntry* pe = ls2_entry(tab, mb, e);
   const uint64_t ctl = ls2_ctl(mb);
@@ -538,9 +548,10 @@ __device__ __forceinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st,
     }
     leave = !pe->bounded;
   }
+  bool killed = false;
   if (__hip_atomic_load(&mb->kill[pe->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == pe->gen) {
     ls2_kill(st, mb, pe->slot, pe->gen, tab->counted != 0);  // relay
-    leave = true;
+    leave = killed = true;
   }
   if (!leave && !pe->bounded && nd > 0) {
     const unsigned long long mine = ls2_wgs(st, pe->slot);
@@ -550,7 +561,7 @@ __device__ __forceinline__ bool ls2_poll(const PoolTable* tab, PoolDevState* st,
       leave = load_dead(st, q->slot) < q->gen && ls2_wgs(st, q->slot) + 2 <= mine;
     }
   }
-  return leave;
+  return (leave ? 1u : 0u) | (killed ? 2u : 0u);
 }
 
 // Wave 0 (every lane): the entry the workgroup works on next, joined; kNoEntry if none can be.  At
@@ -666,7 +677,12 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
         done += 64;
       }
       const uint64_t hits = __ballot(hit);
-      bool leave = hits != 0;
+      // why the workgroup must leave the entry, as a stop-request kind (0 = not at all; the time budget files
+      // kind 0 = end the launch): 1 = the entry was over before this hash started (its dead word), 2 = it is
+      // over since this hash (a win; a kill read by this wave's poll), 3 = leave for another reason (a yield,
+      // a move to a new entry).  The smallest kind of the earliest iteration wins, so the exit knows how many
+      // of the workgroup's last hashes started after it knew the entry was over: 2 for kind 1, 1 for kind 2.
+      uint32_t why = hits != 0 ? 2u : 0u;
       if (__builtin_expect(hits != 0, 0)) {
         const int wl = __builtin_ctzll(hits);
         const uint64_t wn = readlane64(nonce, wl), wval = readlane64(value, wl);
@@ -679,16 +695,17 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
         }
       }
       if (__builtin_expect(((it0 + w) & poll_mask) == 0, 0)) {
-        if (lane == 0) s_flag[wv] = ls2_poll(tab, st, mb, e, &s_seen) ? 1u : 0u;  // the wave's own word
+        if (lane == 0) s_flag[wv] = ls2_poll(tab, st, mb, e, &s_seen);  // the wave's own word
         lds_drain();
-        leave = leave || __builtin_amdgcn_readfirstlane(
-                             __hip_atomic_load(&s_flag[wv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT)) != 0;
+        const uint32_t p = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(&s_flag[wv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
+        why = (p & 2u) ? 2u : (why ? why : (p ? 3u : 0u));
       }
-      leave = leave || readlane64(dead, 0) == gen;
+      if (readlane64(dead, 0) == gen) why = 1u;
       const bool late = budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget;
-      if (__builtin_expect(leave || late, 0)) {
+      if (__builtin_expect(why != 0 || late, 0)) {
         if (lane == 0)
-          __hip_atomic_fetch_min(&s_stop[sw], (it << 1) | (late ? 0u : 1u), __ATOMIC_RELAXED,
+          __hip_atomic_fetch_min(&s_stop[sw], (it << 2) | (late ? 0u : why), __ATOMIC_RELAXED,
                                  __HIP_MEMORY_SCOPE_WORKGROUP);
         lds_drain();
       }
@@ -699,7 +716,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       // all waves see the same set and leave together, one hash after the request.
       const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(verdict);
       if (v != ~0u) {
-        end = (v & 1) == 0;
+        end = (v & 3u) == 0;
         break;
       }
       __builtin_amdgcn_s_barrier();
@@ -712,7 +729,18 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       uint32_t sum = lane < kLsWaves ? s_done[lane] : 0u;
 #pragma unroll
       for (int m = kLsWaves / 2; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
-      ls2_leave_wave(st, mb, c.slot, c.gen, sum, counted);
+      // device-side overshoot: the workgroup's hashes of this entry that started after one of its waves knew
+      // the entry was over -- a request filed after hash i ends the loop after hash i + 1, so 2 such hashes per
+      // wave when the dead word was already up before hash i (kind 1), 1 when hash i itself revealed it (kind 2).
+      // Every wave of the workgroup leaves at the same iteration; capped by the workgroup's count.
+      // (read back from LDS after the barrier above rather than kept in a register through the loop: one more
+      // value live across the loop spilled to scratch)
+      const uint32_t v = __builtin_amdgcn_readfirstlane(
+          __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+      const uint32_t kind = v != ~0u && (v >> 2) + 1u == it ? (v & 3u) : 0u;  // the loop ended on this request
+      uint32_t late_n = kind == 1u ? 2u * 64u * kLsWaves : (kind == 2u ? 64u * kLsWaves : 0u);
+      late_n = late_n < sum ? late_n : sum;
+      ls2_leave_wave(st, mb, c.slot, c.gen, sum, late_n, counted);
     }
     if (it >= iters || end || !counted) break;  // an uncounted launch has no other entry
     if (wv == 0) {
@@ -729,22 +757,6 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   clk_end_ls2(tab, mb, t_start, wv);
 }
 
-// NPOW_LS2_PRIO (A/B builds, tools/experiments/setprio_ab.py; 0 = off): a static s_setprio 1 before
-// the loop for one half of the waves -- 1: the second-dispatched workgroup of each CU (blockIdx.x >=
-// gridDim.x / 2), 2: waves 8..15 of every workgroup, 3: waves 0..7 (control for 2).
-#ifndef NPOW_LS2_PRIO
-#define NPOW_LS2_PRIO 0
-#endif
-__device__ __forceinline__ void ls2_static_prio() {
-#if NPOW_LS2_PRIO == 1
-  if (blockIdx.x >= gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
-#elif NPOW_LS2_PRIO == 2
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) >= kLsWaves / 2) __builtin_amdgcn_s_setprio(1);
-#elif NPOW_LS2_PRIO == 3
-  if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) < kLsWaves / 2) __builtin_amdgcn_s_setprio(1);
-#endif
-}
-
 template <bool BOUNDED>
 __global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2(const PoolTable* __restrict__ tab,
                                                                    PoolDevState* __restrict__ st,
@@ -752,7 +764,6 @@ __global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2(const PoolTa
   uint64_t t_start;
   asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_start) :: "memory");
   clk_begin_lds();
-  ls2_static_prio();
   pool_body_ls2<BOUNDED>(tab, st, mb, t_start);  // records the clock at its end (clk_end_ls2)
 }
 
@@ -765,7 +776,6 @@ __global__ __launch_bounds__(kLsBlock, 8) void npow_pool_kernel_ls2_arg(const Po
   (void)targ;
   const PoolTable* tab = (const PoolTable*)__builtin_amdgcn_kernarg_segment_ptr();
   clk_begin_lds();
-  ls2_static_prio();
   pool_body_ls2<BOUNDED>(tab, st, mb, t_start);  // records the clock at its end (clk_end_ls2)
 }
 

@@ -57,12 +57,11 @@
 #include <unordered_map>
 #include <vector>
 
-#include "npow_host.h"
+#include "npow_pool.h"
 
 namespace npow {
 namespace {
 
-constexpr int kPending = 100;  // job status before it is decided
 constexpr double kYieldMinUs = 1500.0;  // yield a running launch only if more budget than this is left
 // ... and only if it holds fewer live unbounded jobs than this.  A new job then waits at most one
 // launch budget (20 ms), small beside its time-to-work when it shares the GPU with 8+ others
@@ -84,9 +83,6 @@ const double g_poll_us = [] {
 }();
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
 const bool g_trace_lat = getenv("NANOPOW_TRACE_LATENCY") != nullptr;
-double now_us() {
-  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
-}
 // Fault injection (tests): see the header comment.
 struct Faults {
   uint64_t invalid_mask = 0;  // logical devices whose wins read back corrupted
@@ -137,67 +133,18 @@ const Faults& faults() {
     if (g_debug) fprintf(stderr, __VA_ARGS__); \
   } while (0)
 
-// [base, base + count) mod 2^64: nonces of a job still to be handed to launches
-struct Range {
-  uint64_t base, count;
-};
+}  // namespace
 
-struct Job {
-  uint64_t ticket = 0;
-  RootPrecomp pre{};
-  uint64_t u[NPOW_ASM_N_UNIFORMS] = {};
-  uint64_t threshold = 0, start = 0, max_per_dev = 0, spacing = 0;
-  const volatile uint32_t* cancel = nullptr;
-  std::vector<int> devs;  // device ids; the k-th starts on [start + k * spacing, + stride)
-  // guarded by g_pool.mu
-  std::vector<std::deque<Range>> todo;  // per device k: ranges not yet handed to a launch (a dead
-                                        // device's remainder is re-strided onto the survivors')
-  std::vector<uint8_t> on_dev;      // per device k: a slot holds the job
-  std::vector<uint8_t> seen_dev;    // per device k: adopted at least once (re-adoptions do not yield)
-  std::vector<uint8_t> dev_done;    // per device k: finished with the job
-  std::vector<int> dev_slot;        // per device k: the slot holding it while on_dev[k] ...
-  std::vector<uint64_t> dev_gen;    // ... and its generation there (the decider raises their kill words)
-  std::vector<double> t_stop;       // per device k: when its worker saw it stop hashing the job (us; 0 = never adopted)
-  int winner_k = -1;                // the device whose result decided the job
-  int pending_devs = 0;
-  bool admitted = false;
-  bool lost = false;                // a dead device's remainder had no surviving device to go to
-  int lost_code = NPOW_ERR_HIP;
-  std::atomic<bool> finished{false};  // written under g_pool.mu; waiters may spin on it
-  std::condition_variable cv;         // its waiters (pool_wait), notified by finish_locked: one job's end
-                                      // wakes only its own waiters, not every thread blocked in npow_wait
-  int status = kPending;
-  uint64_t nonce = 0, value = 0, done = 0;
-  std::string err;
-  // lock-free flags the workers poll
-  std::atomic<bool> decided{false};
-  std::atomic<bool> cancel_req{false};
-
-  bool cancel_seen() const { return cancel_req.load(std::memory_order_relaxed) || (cancel && load_acquire(cancel)); }
-  // host timestamps of the job's life (steady clock, us): t_submit, t_decide and t_finish always
-  // (npow_wait_info), the rest for NANOPOW_TRACE_LATENCY, which prints them in pool_wait
-  double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0, t_decide = 0;
-};
-using JobP = std::shared_ptr<Job>;
-
-struct Pool {
-  std::mutex mu;
-  std::condition_variable cv_work;  // workers: new admissions / shutdown
-  std::deque<JobP> waiting;
-  std::vector<JobP> active;
-  std::unordered_map<uint64_t, JobP> tickets;
-  uint64_t next_ticket = 1;
-  uint32_t max_active = kMaxSlots;
-  bool running = false;
-  std::atomic<uint64_t> version{0};  // bumped whenever `active` gains a job
-  std::atomic<uint64_t> decisions{0};  // bumped when a job split over devices is decided: wakes napping workers
-} g_pool;
-
+// -- jobs shared with the CPU workers (npow_pool.h) ---------------------------------------------
+double now_us() {
+  return std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+Pool g_pool;
 std::atomic<uint64_t> g_gen{0};
 std::atomic<bool> g_exiting{false};  // process exit: workers leave at once, no further HIP calls
 
 // -- job state transitions (caller holds g_pool.mu) ------------------------------------------
-void decide_locked(Job& j, int status, uint64_t nonce = 0, uint64_t value = 0) {
+void decide_locked(Job& j, int status, uint64_t nonce, uint64_t value) {
   if (j.status != kPending) return;
   j.status = status;
   j.nonce = nonce;
@@ -255,9 +202,13 @@ void abandon_locked(const JobP& j, size_t k, int code, const std::string& msg) {
   std::deque<Range> rest;
   rest.swap(j->todo[k]);
   if (!j->decided && !rest.empty()) {
-    std::vector<size_t> surv;
-    for (size_t k2 = 0; k2 < j->devs.size(); ++k2)
-      if (k2 != k && !g_devs[(size_t)j->devs[k2]]->dead) surv.push_back(k2);
+    // the surviving GPUs take it; the CPU device (npow_cpu.cpp) only when no GPU of the job is left
+    std::vector<size_t> surv, surv_cpu;
+    for (size_t k2 = 0; k2 < j->devs.size(); ++k2) {
+      const Device& d2 = *g_devs[(size_t)j->devs[k2]];
+      if (k2 != k && !d2.dead) (d2.cpu_threads ? surv_cpu : surv).push_back(k2);
+    }
+    if (surv.empty()) surv.swap(surv_cpu);
     if (surv.empty()) {
       j->lost = true;
       j->lost_code = code;
@@ -293,7 +244,8 @@ void abandon_locked(const JobP& j, size_t k, int code, const std::string& msg) {
 void stop_other_devices_locked(Job& j, size_t k_win) {
   if (j.devs.size() < 2) return;
   for (size_t k = 0; k < j.devs.size(); ++k) {
-    if (k == k_win || !j.on_dev[k] || j.dev_slot[k] < 0) continue;
+    if (k == k_win || !j.on_dev[k] || j.dev_slot[k] < 0) continue;  // (a CPU device has no slot: its threads
+                                                                      // read the decision themselves)
     Device& d = *g_devs[(size_t)j.devs[k]];
     __atomic_store_n(&d.pmb->kill[j.dev_slot[k]], j.dev_gen[k], __ATOMIC_RELEASE);
     std::lock_guard<std::mutex> sg(d.stats_mu);
@@ -302,6 +254,23 @@ void stop_other_devices_locked(Job& j, size_t k_win) {
   g_pool.decisions.fetch_add(1, std::memory_order_release);
   g_pool.cv_work.notify_all();
 }
+
+int index_in(const Job& j, int dev) {
+  for (size_t k = 0; k < j.devs.size(); ++k)
+    if (j.devs[k] == dev) return (int)k;
+  return -1;
+}
+
+// Needs (under g_pool.mu): some active job wants this device.
+bool wants_device_locked(int dev) {
+  for (const JobP& j : g_pool.active) {
+    const int k = index_in(*j, dev);
+    if (k >= 0 && !j->on_dev[k] && !j->dev_done[k]) return true;
+  }
+  return false;
+}
+
+namespace {
 
 // -- one device's worker ------------------------------------------------------------------------
 enum class SlotState { kFree, kActive, kDraining };
@@ -312,6 +281,7 @@ struct Slot {
   size_t k = 0;            // the device's index within job->devs
   uint64_t gen = 0;
   uint64_t baseline = 0;   // done counter of this slot index at its last retirement
+  uint64_t late_base = 0;  // ... and its late counter (kLateWord)
   bool win_seen = false;
   bool requeue = false;    // invalid GPU result: hand the job back to this device after retiring
   bool no_more = false;    // bounded range fully issued
@@ -387,21 +357,6 @@ class Worker {
   int step();
   void nap();
 };
-
-int index_in(const Job& j, int dev) {
-  for (size_t k = 0; k < j.devs.size(); ++k)
-    if (j.devs[k] == dev) return (int)k;
-  return -1;
-}
-
-// Needs (under g_pool.mu): some active job wants this device.
-bool wants_device_locked(int dev) {
-  for (const JobP& j : g_pool.active) {
-    const int k = index_in(*j, dev);
-    if (k >= 0 && !j->on_dev[k] && !j->dev_done[k]) return true;
-  }
-  return false;
-}
 
 void Worker::adopt() {
   if (d_.dead) return;  // draining before it releases its jobs (run())
@@ -662,6 +617,7 @@ void Worker::early_finish(int s) {
   sl.fin_seen = true;
   if (win_published(s)) handle_win(s);  // the winner released its record before closing the entry
   const uint64_t total = __atomic_load_n(&d_.pmb->fin[s].total, __ATOMIC_RELAXED);
+  const uint64_t late = __atomic_load_n(&d_.pmb->fin[s].late, __ATOMIC_RELAXED);
   std::lock_guard<std::mutex> g(g_pool.mu);
   Job& j = *sl.job;
   if (d_.dead || sl.requeue || !j.decided.load()) return;
@@ -669,6 +625,12 @@ void Worker::early_finish(int s) {
   const uint64_t delta = total - sl.baseline;
   sl.baseline = total;  // retire() then reads back the same total: a delta of 0
   j.done += delta;
+  j.late[sl.k] += late - sl.late_base;
+  {
+    std::lock_guard<std::mutex> sg(d_.stats_mu);
+    d_.late += late - sl.late_base;
+  }
+  sl.late_base = late;
   if (g_trace_lat && j.t_kend == 0) j.t_kend = now_us();
   {
     std::lock_guard<std::mutex> sg(d_.stats_mu);
@@ -696,18 +658,17 @@ void Worker::check_slots() {
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);
       sl.state = SlotState::kDraining;
     } else if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {
-      bool started = false;  // has any launch holding the job begun on the GPU?
-      for (const Slot::Issued& r : sl.inflight) started = started || launch_started(r.seq);
       {
         std::lock_guard<std::mutex> g(g_pool.mu);
         if (!j.decided.load()) {
           j.cancel_req = true;
           decide_locked(j, NPOW_CANCELLED);
         }
-        // queued behind another launch only: this device hashes nothing of the job after the decision
-        // (a one-job launch starting after the kill leaves at once; others see it within an iteration)
-        if (!started && j.t_decide > 0 && j.t_stop[sl.k] == 0) j.t_stop[sl.k] = j.t_decide;
       }
+      // The job's stop time (Job::t_stop) is taken when this worker sees it stop hashing: its final
+      // count published, or the launches that held it retired (device_done_locked).  A launch queued
+      // behind another and started after the kill still hashes the job until one of its waves polls
+      // the kill word (within an iteration), so "not started at the decision" is no proof of zero.
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);  // in-flight waves stop
       sl.state = SlotState::kDraining;
       sl.stop_us = now_us();
@@ -853,7 +814,9 @@ int Worker::retire() {
       if (win_published(s)) handle_win(s);
       size_t m = 0;
       while (m < sl.inflight.size() && sl.inflight[m].seq <= seq) ++m;
-      if (sl.job && sl.job->max_per_dev)  // dense bounded ranges, hashed in full (fail_all's accounting)
+      // dense bounded ranges, hashed in full (fail_all's accounting) -- unless the slot's generation has
+      // stopped (won or killed): its launches may have ended part-way, so nothing more is credited
+      if (sl.job && sl.job->max_per_dev && !sl.win_seen && sl.stop_us == 0)
         for (size_t i = 0; i < m; ++i) sl.unread += sl.inflight[i].count;
       sl.inflight.erase(sl.inflight.begin(), sl.inflight.begin() + (ptrdiff_t)m);
     }
@@ -874,13 +837,18 @@ int Worker::retire() {
     if (e == hipErrorNotReady) continue;
     if (e != hipSuccess) return fail(NPOW_ERR_HIP, std::string("pool read-back: ") + hipGetErrorString(e));
     // every launch that held the slot has completed: its done shards are final
-    uint64_t sum = 0;
-    for (int i = 0; i < kPoolDoneShards; ++i) sum += d_.h_done[(size_t)s * row + i * 8];
-    const uint64_t delta = sum - sl.baseline;
+    uint64_t sum = 0, late = 0;
+    for (int i = 0; i < kPoolDoneShards; ++i) {
+      sum += d_.h_done[(size_t)s * row + i * 8];
+      late += d_.h_done[(size_t)s * row + i * 8 + kLateWord];
+    }
+    const uint64_t delta = sum - sl.baseline, late_delta = late - sl.late_base;
     sl.baseline = sum;
+    sl.late_base = late;
     {
       std::lock_guard<std::mutex> sg(d_.stats_mu);
       d_.nonces += delta;
+      d_.late += late_delta;
     }
     if (win_published(s)) handle_win(s);  // published by the last launch, not yet seen
     NPOW_DBG("nanopow[%d]: retire slot %d g%llu done %llu requeue %d early %d\n", d_.id, s,
@@ -896,6 +864,7 @@ int Worker::retire() {
       std::lock_guard<std::mutex> g(g_pool.mu);
       Job& j = *sl.job;
       j.done += delta;
+      j.late[sl.k] += late_delta;
       if (d_.dead) {
         abandon_locked(sl.job, sl.k, d_.dead_code, d_.dead_msg);  // survivors take what is left
       } else if (!j.decided && (sl.requeue || !j.todo[sl.k].empty())) {
@@ -925,9 +894,13 @@ void Worker::fail_all(const std::string& msg) {
     if (sl.state == SlotState::kFree) continue;
     if (sl.job->max_per_dev) {
       // no read-back from a failed device: the job counts its bounded ranges that completed here
-      // (each hashed in full, dense) from their sizes; the rest go back to it and are re-strided
+      // (each hashed in full, dense) from their sizes; the rest go back to it and are re-strided.
+      // Exact for a job that ends without a hit; once the slot's generation has stopped (a win, a kill)
+      // its last launches may have ended part-way, so only the ranges retired before that are counted
+      // (crediting them in full over-counted a won job): a lower bound then.
       const uint64_t kept = push_back_locked(sl, 0, true);
-      if (!sl.early) sl.job->done += sl.unread + kept;
+      const bool stopped = sl.win_seen || sl.stop_us > 0;
+      if (!sl.early) sl.job->done += sl.unread + (stopped ? 0 : kept);
     }
     abandon_locked(sl.job, sl.k, d_.dead_code, d_.dead_msg);
     sl.job.reset();
@@ -1101,6 +1074,10 @@ void pool_start() {
   }
   for (auto& dp : g_devs) {
     Device* d = dp.get();
+    if (d->cpu_threads) {
+      d->worker = std::thread([d] { cpu_worker_run(*d); });
+      continue;
+    }
     d->worker = std::thread([d] {
       Worker w(*d);
       w.run();
@@ -1164,6 +1141,7 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   j->dev_slot.assign(G, -1);
   j->dev_gen.assign(G, 0);
   j->t_stop.assign(G, 0.0);
+  j->late.assign(G, 0);
   j->pending_devs = (int)G;
   j->t_submit = now_us();
   std::lock_guard<std::mutex> g(g_pool.mu);
@@ -1220,6 +1198,11 @@ int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* va
       }
     info->stop_after_decide_us = worst;
     info->overshoot_nonces = (uint64_t)over;
+    uint64_t dev_late = 0;
+    for (size_t k = 0; k < j->devs.size(); ++k)
+      if ((int)k != j->winner_k) dev_late += j->late[k];
+    info->late_nonces_losers = dev_late;
+    info->late_nonces_winner = j->winner_k >= 0 ? j->late[(size_t)j->winner_k] : 0;
   }
   if (g_trace_lat)
     fprintf(stderr, "nanopow-lat adopt %.1f launch %.1f win %.1f kend %.1f finish %.1f return %.1f\n",

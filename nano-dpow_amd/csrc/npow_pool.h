@@ -1,0 +1,95 @@
+// npow_pool.h -- the work pool's jobs and their state transitions, shared by the GPU workers
+// (npow_pool.cpp) and the CPU workers (npow_cpu.cpp, `--cpu-threads`).  Internal to libnanopow.so.
+#pragma once
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "npow_host.h"
+
+namespace npow {
+
+constexpr int kPending = 100;  // job status before it is decided
+double now_us();               // steady clock, microseconds
+
+// [base, base + count) mod 2^64: nonces of a job still to be handed to launches
+struct Range {
+  uint64_t base, count;
+};
+
+struct Job {
+  uint64_t ticket = 0;
+  RootPrecomp pre{};
+  uint64_t u[NPOW_ASM_N_UNIFORMS] = {};
+  uint64_t threshold = 0, start = 0, max_per_dev = 0, spacing = 0;
+  const volatile uint32_t* cancel = nullptr;
+  std::vector<int> devs;  // device ids; the k-th starts on [start + k * spacing, + stride)
+  // guarded by g_pool.mu
+  std::vector<std::deque<Range>> todo;  // per device k: ranges not yet handed to a launch (a dead
+                                        // device's remainder is re-strided onto the survivors')
+  std::vector<uint8_t> on_dev;      // per device k: a slot holds the job
+  std::vector<uint8_t> seen_dev;    // per device k: adopted at least once (re-adoptions do not yield)
+  std::vector<uint8_t> dev_done;    // per device k: finished with the job
+  std::vector<int> dev_slot;        // per device k: the slot holding it while on_dev[k] ...
+  std::vector<uint64_t> dev_gen;    // ... and its generation there (the decider raises their kill words)
+  std::vector<double> t_stop;       // per device k: when its worker saw it stop hashing the job (us; 0 = never adopted)
+  std::vector<uint64_t> late;       // per device k: nonces its waves hashed after they knew the job was over
+                                    // (device-side count, PoolDevState kLateWord)
+  int winner_k = -1;                // the device whose result decided the job
+  int pending_devs = 0;
+  bool admitted = false;
+  bool lost = false;                // a dead device's remainder had no surviving device to go to
+  int lost_code = NPOW_ERR_HIP;
+  std::atomic<bool> finished{false};  // written under g_pool.mu; waiters may spin on it
+  std::condition_variable cv;         // its waiters (pool_wait), notified by finish_locked: one job's end
+                                      // wakes only its own waiters, not every thread blocked in npow_wait
+  int status = kPending;
+  uint64_t nonce = 0, value = 0, done = 0;
+  std::string err;
+  // lock-free flags the workers poll
+  std::atomic<bool> decided{false};
+  std::atomic<bool> cancel_req{false};
+
+  bool cancel_seen() const { return cancel_req.load(std::memory_order_relaxed) || (cancel && load_acquire(cancel)); }
+  // host timestamps of the job's life (steady clock, us): t_submit, t_decide and t_finish always
+  // (npow_wait_info), the rest for NANOPOW_TRACE_LATENCY, which prints them in pool_wait
+  double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0, t_decide = 0;
+};
+using JobP = std::shared_ptr<Job>;
+
+struct Pool {
+  std::mutex mu;
+  std::condition_variable cv_work;  // workers: new admissions / shutdown
+  std::deque<JobP> waiting;
+  std::vector<JobP> active;
+  std::unordered_map<uint64_t, JobP> tickets;
+  uint64_t next_ticket = 1;
+  uint32_t max_active = kMaxSlots;
+  bool running = false;
+  std::atomic<uint64_t> version{0};  // bumped whenever `active` gains a job
+  std::atomic<uint64_t> decisions{0};  // bumped when a job split over devices is decided: wakes napping workers
+};
+extern Pool g_pool;  // npow_pool.cpp
+
+extern std::atomic<uint64_t> g_gen;      // slot generations (unique, > 0)
+extern std::atomic<bool> g_exiting;      // process exit: workers leave at once, no further HIP calls
+
+// -- job state transitions (caller holds g_pool.mu; npow_pool.cpp) ------------------------------
+void decide_locked(Job& j, int status, uint64_t nonce = 0, uint64_t value = 0);
+void admit_locked();
+void finish_locked(const JobP& j);
+void device_done_locked(const JobP& j, size_t k);
+void abandon_locked(const JobP& j, size_t k, int code, const std::string& msg);
+void stop_other_devices_locked(Job& j, size_t k_win);
+int index_in(const Job& j, int dev);  // the job's index of logical device dev, or -1
+bool wants_device_locked(int dev);    // some active job wants this device
+
+// -- CPU workers (npow_cpu.cpp) ------------------------------------------------------------------
+void cpu_worker_run(Device& d);  // the pool worker of a CPU device (Device::cpu_threads > 0)
+
+}  // namespace npow

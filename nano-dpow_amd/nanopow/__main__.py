@@ -8,7 +8,8 @@ client/README.md:31):
   -g/--gpu PLATFORM:DEVICE[:THREADS]   repeatable; PLATFORM is ignored (HIP has one); THREADS
                                 (nonces per launch in the reference, default 1048576) is a lower
                                 bound on a search launch's nonces (see apply_threads)
-  -c/--cpu-threads N            rejected: this engine runs on MI355X GPUs only
+  -c/--cpu-threads N            N CPU worker threads beside the GPUs (one more device of the work pool:
+                                every request also gets a stride hashed on the host; default 0)
   --gpu-local-work-size N       accepted and ignored (search workgroups are 512 lanes on gfx950)
   --shuffle                     pick a random queued request instead of the oldest
   --max-active N                requests searched at once by the GPU work pool (default 4)
@@ -32,7 +33,7 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("-g", "--gpu", action="append", default=[], metavar="PLATFORM:DEVICE:THREADS",
                     help="Specifies which GPU(s) to use. THREADS is optional and defaults to 1048576.")
     ap.add_argument("-c", "--cpu-threads", "--cpu_threads", dest="cpu_threads", type=int, default=0,
-                    metavar="THREADS", help="Not supported: this engine runs on GPUs only.")
+                    metavar="THREADS", help="Specifies how many CPU threads to use (beside the GPUs).")
     ap.add_argument("--gpu-local-work-size", "--gpu_local_work_size", dest="local_work_size", type=int,
                     default=None, metavar="N", help="Accepted for compatibility; gfx950 workgroups are fixed.")
     ap.add_argument("--shuffle", action="store_true",
@@ -70,12 +71,10 @@ def apply_threads(eng, gpus) -> int:
     return 0
 
 
-def main(argv=None) -> int:
-    args = parse_args(argv)
-    logging.basicConfig(level=logging.DEBUG if args.verbose else logging.INFO,
-                        format="%(asctime)s %(levelname)s %(message)s")
-    if args.cpu_threads:
-        print("CPU workers are not supported by this engine: use --gpu PLATFORM:DEVICE", file=sys.stderr)
+def build(args: argparse.Namespace):
+    """The configured HttpWorkServer (not yet serving), or an exit status (int) after printing why not."""
+    if not 0 <= args.cpu_threads <= 1024:
+        print("--cpu-threads must be in [0, 1024]", file=sys.stderr)
         return 2
     try:
         base = W.parse_threshold(args.base_difficulty)
@@ -87,16 +86,20 @@ def main(argv=None) -> int:
         print(f"Failed to parse options: {e}", file=sys.stderr)
         return 2
 
-    from ._lib import engine  # loads libnanopow.so; raises if it or the GPU is missing
+    from . import _lib  # loads libnanopow.so on first use; raises if it or the GPU is missing
     from .server import HttpWorkServer, WorkServer
 
-    eng = engine()
+    # CPU workers run beside the GPUs only: the engine still refuses to start without a GPU
+    eng = _lib.engine(cpu_threads=args.cpu_threads)
+    n_gpus = bin(eng.gpu_mask).count("1")
     mask = 0
     for _platform, device, _threads in gpus:
-        if device >= eng.n_devices:
-            print(f"GPU {device} not found ({eng.n_devices} visible)", file=sys.stderr)
+        if device >= n_gpus:
+            print(f"GPU {device} not found ({n_gpus} visible)", file=sys.stderr)
             return 2
         mask |= 1 << device
+    if mask and eng.cpu_device is not None:
+        mask |= 1 << eng.cpu_device  # the selected GPUs and the CPU workers
     if not 1 <= args.max_active <= 64:
         print("--max-active must be in [1, 64]", file=sys.stderr)
         return 2
@@ -104,8 +107,19 @@ def main(argv=None) -> int:
     srv = HttpWorkServer(WorkServer(eng, base_threshold=base, shuffle=args.shuffle, device_mask=mask,
                                     max_active=args.max_active), host, port_i)
     logging.info("Configured for the live network with threshold %016x", base)
-    logging.info("Ready to receive requests on %s (%d GPU(s), %s)", srv.address,
-                 bin(mask).count("1") if mask else eng.n_devices, eng.version())
+    logging.info("Ready to receive requests on %s (%d GPU(s)%s, %s)", srv.address,
+                 bin(mask & eng.gpu_mask).count("1") if mask else n_gpus,
+                 f" + {args.cpu_threads} CPU thread(s)" if eng.cpu_device is not None else "", eng.version())
+    return srv
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    logging.basicConfig(level=logging.DEBUG if args.verbose else logging.INFO,
+                        format="%(asctime)s %(levelname)s %(message)s")
+    srv = build(args)
+    if isinstance(srv, int):
+        return srv
     try:
         srv.serve_forever()
     except KeyboardInterrupt:

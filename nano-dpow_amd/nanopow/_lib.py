@@ -30,9 +30,9 @@ NPOW_ERR_INVALID_WORK = -5
 NPOW_ERR_CAPACITY = -6
 NPOW_ERR_INTERNAL = -7
 
-NPOW_ABI_VERSION = 3
+NPOW_ABI_VERSION = 4
 # hash paths of npow_values_path
-NPOW_PATH_SEARCH = 0   # the stream the search and sweep kernels execute (two lockstep workgroups per CU)
+NPOW_PATH_SEARCH = 0   # the stream the search and sweep kernels execute (four 512-lane workgroups per CU)
 NPOW_PATH_SEQ = 1      # a second generated stream, scheduled without barriers
 NPOW_PATH_GENERIC = 2  # plain HIP C++ of the 12 rounds, one (root, nonce) per lane
 
@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "npow_device_stats_get", "npow_device_stats_reset", "npow_version",
     "npow_submit", "npow_wait", "npow_cancel", "npow_pool_config", "npow_pool_status",
     "npow_set_pool_tuning", "npow_values_path", "npow_wait_info", "npow_device_stats_get_sized",
-    "npow_abi_version",
+    "npow_abi_version", "npow_config_cpu_threads",
 )
 
 
@@ -74,6 +74,9 @@ class DeviceStats(ctypes.Structure):
         ("yields", ctypes.c_uint64),
         ("dyn_entries", ctypes.c_uint64),
         ("kills_relayed", ctypes.c_uint64),  # ABI 3
+        ("late_nonces", ctypes.c_uint64),    # ABI 4
+        ("hip_device", ctypes.c_int32),
+        ("cu_first", ctypes.c_int32),
     ]
 
 
@@ -91,6 +94,8 @@ class SearchInfo(ctypes.Structure):
         ("finish_us", ctypes.c_double),
         ("stop_after_decide_us", ctypes.c_double),
         ("overshoot_nonces", ctypes.c_uint64),
+        ("late_nonces_losers", ctypes.c_uint64),  # ABI 4: counted on the devices
+        ("late_nonces_winner", ctypes.c_uint64),
     ]
 
 
@@ -177,6 +182,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             lib.npow_device_stats_get_sized.restype = ctypes.c_int
             lib.npow_abi_version.argtypes = []
             lib.npow_abi_version.restype = ctypes.c_int
+        if hasattr(lib, "npow_config_cpu_threads"):  # ABI 4
+            lib.npow_config_cpu_threads.argtypes = [u32]
+            lib.npow_config_cpu_threads.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -285,11 +293,21 @@ class Ticket:
 class Engine:
     """Thin object wrapper over the C ABI (one per process is enough)."""
 
-    def __init__(self, path: str = LIB_PATH) -> None:
+    def __init__(self, path: str = LIB_PATH, cpu_threads: int = 0) -> None:
+        """cpu_threads > 0: add that many CPU worker threads as one more logical device after the GPUs
+        (npow_config_cpu_threads; the reference work server's --cpu-threads).  It only takes effect in
+        the process's first Engine (npow_init is process-wide)."""
         self.lib = load(path)
+        if cpu_threads:
+            _check(self.lib.npow_config_cpu_threads(cpu_threads), self.lib)
         n = ctypes.c_int(0)
         _check(self.lib.npow_init(ctypes.byref(n)), self.lib)
         self.n_devices = n.value
+        self.cpu_device = None  # logical id of the CPU workers' device, if any
+        for d in range(self.n_devices):
+            if self.stats(d).hip_device < 0:
+                self.cpu_device = d
+        self.gpu_mask = ((1 << self.n_devices) - 1) & ~(0 if self.cpu_device is None else 1 << self.cpu_device)
 
     # -- CPU helpers -------------------------------------------------------------------
     def work_value(self, root: bytes, nonce: int) -> int:
@@ -437,10 +455,11 @@ _engine: Optional[Engine] = None
 _engine_lock = threading.Lock()
 
 
-def engine() -> Engine:
-    """Process-wide engine (initialised on first use; raises if no GPU)."""
+def engine(cpu_threads: int = 0) -> Engine:
+    """Process-wide engine (initialised on first use; raises if no GPU).  cpu_threads: CPU workers
+    beside the GPUs (Engine), honoured by the first call only."""
     global _engine
     with _engine_lock:
         if _engine is None:
-            _engine = Engine()
+            _engine = Engine(cpu_threads=cpu_threads)
         return _engine

@@ -52,12 +52,17 @@ class OracleEngine:
         self.calls = []
         self.lock = threading.Lock()
         self._stats = [dict(nonces=0, launches=0, kernel_ms=0.0) for _ in range(n_devices)]
+        self.cpu_device, self.gpu_mask = None, (1 << n_devices) - 1
 
     def stats(self, device=0):
         st = self._stats[device]
         return SimpleNamespace(kernel_ms=st["kernel_ms"], nonces=st["nonces"], launches=st["launches"],
                                clock_mhz=0.0, early_finishes=0, kills_relayed=0, host_cpu_ms=0.0,
-                               host_wall_ms=1.0)
+                               host_wall_ms=1.0, grid=0, pool_groups=4, late_nonces=0, hip_device=0,
+                               cu_first=-1)
+
+    def version(self):
+        return "oracle stand-in engine (tests/fake_engine.py)"
 
     def reset_stats(self, device=0):
         self._stats[device] = dict(nonces=0, launches=0, kernel_ms=0.0)

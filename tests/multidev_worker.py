@@ -1,6 +1,7 @@
-"""Child process of tests/test_gpu_multidevice.py (run with NANOPOW_VIRTUAL_DEVICES=4): the
-multi-device first-win path on one physical GPU exposed as 4 logical devices, each with its own
-stream, buffers and pool worker.  Prints one JSON line; exits non-zero on any mismatch."""
+"""Child process of tests/test_gpu_multidevice.py: the multi-device first-win path, on one physical GPU
+exposed as NANOPOW_VIRTUAL_DEVICES logical devices (each a CU partition with its own stream, buffers
+and pool worker) or on every physical GPU of the box (EXPECT_DEVICES).  Argument "burst": only a burst
+of 64 roots split over every device.  Prints one JSON line; exits non-zero on any mismatch."""
 import json
 import os
 import random
@@ -18,11 +19,46 @@ M64 = (1 << 64) - 1
 RECEIVE, LOW = 0xfffffe0000000000, 0xfffff00000000000
 
 
+def partitions(eng, G):
+    """[hip_device, cu_first, cus] per logical device; logical devices sharing a HIP device must hold
+    disjoint CU ranges that cover it (NANOPOW_VIRTUAL_DEVICES: CU-masked streams, npow_engine.cpp)."""
+    parts = [[eng.stats(d).hip_device, eng.stats(d).cu_first, eng.stats(d).cus] for d in range(G)]
+    by_dev = {}
+    for hip, first, cus in parts:
+        by_dev.setdefault(hip, []).append((first, cus))
+    for hip, lst in by_dev.items():
+        if len(lst) > 1 and all(f >= 0 for f, _ in lst):
+            lst.sort()
+            assert all(a[0] + a[1] == b[0] for a, b in zip(lst, lst[1:])), lst  # disjoint, contiguous
+            assert len({c for _, c in lst}) == 1, lst                            # equal shares
+    return parts
+
+
+def burst(eng, G, n=64):
+    """n roots in flight at once, each split over every device: all valid (hashlib)."""
+    rng = random.Random(17)
+    roots = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(n)]
+    ts = [eng.submit(rt, RECEIVE, start=rng.getrandbits(64), device_mask=0) for rt in roots]
+    for rt, t in zip(roots, ts):
+        r = t.wait(60)
+        assert r.status == _lib.NPOW_OK and oracle.work_value_hashlib(rt, r.nonce) == r.value >= RECEIVE
+
+
 def main():
     eng = _lib.Engine()
     G = eng.n_devices
-    assert G == int(os.environ["NANOPOW_VIRTUAL_DEVICES"]), G
-    out = {"devices": G}
+    want = os.environ.get("EXPECT_DEVICES") or os.environ.get("NANOPOW_VIRTUAL_DEVICES")
+    assert want is None or G == int(want), G
+    out = {"devices": G, "partitions": partitions(eng, G)}
+    if len(sys.argv) > 1 and sys.argv[1] == "burst":
+        for d in range(G):
+            eng.reset_stats(d)
+        burst(eng, G)
+        out["launches_per_device"] = [eng.stats(d).launches for d in range(G)]
+        assert all(x > 0 for x in out["launches_per_device"]), out
+        out["ok"] = True
+        print(json.dumps(out), flush=True)
+        return
     spacing = (1 << 64) // G
     for d in range(G):
         eng.reset_stats(d)

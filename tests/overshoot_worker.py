@@ -3,7 +3,8 @@
 client/work_handler.py:61-80).  Run with NANOPOW_VIRTUAL_DEVICES=G: searches split over all G
 devices (disjoint strides); for each, npow_wait_info reports when the host accepted the winner and
 how long the other devices kept hashing after that (host-observed upper bound) with the nonces that
-span is worth at each device's kernel rate.  Asserts a valid winner every time and a bound on the
+span is worth at each device's kernel rate, and the nonces the losing devices' waves hashed after they
+knew the job was over, counted in the kernel (late_nonces_losers).  Asserts a valid winner every time and a bound on the
 overshoot; prints one JSON line with the distributions."""
 import json
 import os
@@ -32,7 +33,7 @@ def main(n_search, which):
     G = eng.n_devices
     thr = THRESHOLDS[which]
     rng = random.Random(11)
-    spans, over, done, ttw, winners = [], [], [], [], []
+    spans, over, done, ttw, winners, late_l, late_w = [], [], [], [], [], [], []
     for i in range(n_search):
         root = bytes(rng.getrandbits(8) for _ in range(32))
         t = eng.submit(root, thr, start=rng.getrandbits(64), device_mask=0)
@@ -42,15 +43,23 @@ def main(n_search, which):
         assert info.n_devices == G and 0 <= info.winner_device < G
         spans.append(info.stop_after_decide_us)
         over.append(info.overshoot_nonces)
+        late_l.append(info.late_nonces_losers)
+        late_w.append(info.late_nonces_winner)
         done.append(info.nonces_done)
         ttw.append(info.finish_us)
         winners.append(info.winner_device)
-    kills = sum(eng.stats(d).kills_relayed for d in range(G))
+    st = [eng.stats(d) for d in range(G)]
+    kills = sum(x.kills_relayed for x in st)
     res = {"ok": True, "devices": G, "threshold": which, "searches": n_search,
+           "partition": [[x.hip_device, x.cu_first, x.cus] for x in st],
            "stop_after_decide_us": {"p50": round(pct(spans, 50), 1), "p99": round(pct(spans, 99), 1),
                                     "max": round(max(spans), 1)},
            "overshoot_nonces": {"p50": pct(over, 50), "p99": pct(over, 99),
                                 "mean_over_nonces_done": round(sum(over) / max(1, sum(done)), 5)},
+           # counted in the kernels: the losing devices' hashes after their waves knew the job was over
+           "late_nonces_losers": {"p50": pct(late_l, 50), "p99": pct(late_l, 99),
+                                  "mean_over_nonces_done": round(sum(late_l) / max(1, sum(done)), 5)},
+           "late_nonces_winner": {"p50": pct(late_w, 50), "p99": pct(late_w, 99)},
            "finish_ms_p50": round(pct(ttw, 50) / 1e3, 3),
            "distinct_winners": len(set(winners)), "kills_relayed": kills,
            "mean_nonces_done": round(statistics.mean(done))}

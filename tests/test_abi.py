@@ -65,6 +65,17 @@ def test_uninitialised_calls_fail_cleanly():
     assert lib.npow_last_error()
 
 
+def test_stats_reject_null_out():
+    """npow_device_stats_get / _sized with out == NULL (or size 0) return
+    NPOW_ERR_BAD_ARGUMENT instead of writing through the pointer."""
+    lib = _lib.load()
+    assert lib.npow_device_stats_get(0, None) == _lib.NPOW_ERR_BAD_ARGUMENT
+    assert lib.npow_device_stats_get_sized(0, None, ctypes.sizeof(_lib.DeviceStats)) == _lib.NPOW_ERR_BAD_ARGUMENT
+    st = _lib.DeviceStats()
+    assert lib.npow_device_stats_get_sized(0, ctypes.byref(st), 0) == _lib.NPOW_ERR_BAD_ARGUMENT
+    assert lib.npow_last_error()
+
+
 def test_init_without_gpu_reports_no_device():
     import torch  # noqa: F401  (only to ask whether this host has a GPU)
     if torch.cuda.is_available():

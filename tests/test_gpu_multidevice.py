@@ -1,14 +1,23 @@
-"""Multi-device paths on a one-GPU box: the engine opened with NANOPOW_VIRTUAL_DEVICES=G (G logical
-devices over the physical GPU, each with its own stream, buffers and pool worker) in a child
-process.
-* tests/multidev_worker.py (G = 4): disjoint per-device strides, the winner from the right stride,
-  exact per-device exhaustion, cancellation reaching every device, bursts and sweeps split over
-  devices, subset masks.
-* tests/sweep_split_worker.py (G = 2, 4, 8): BASELINE configs[2] at full size -- the 2^36 sweep of
-  the fixture root split over G devices, bit-exact against tests/golden/sweep_2p36.json, the devices'
+"""Multi-device paths, in child processes (the engine's device set is fixed at npow_init).
+
+On a one-GPU box the engine is opened with NANOPOW_VIRTUAL_DEVICES=G: G logical devices over the
+physical GPU, each a partition of its CUs (a CU-masked stream over 256 / G CUs, the same number on every
+XCD, npow_engine.cpp init_device; profiles/r04_cu_mask_probe.txt) with its own stream, buffers and pool
+worker -- so every device's launch runs from its start on CUs of its own, as on separate GPUs.
+NANOPOW_VIRTUAL_PARTITION=share makes them time-share the whole GPU instead (rounds 1-3).
+* tests/multidev_worker.py (G = 4): the partitions (disjoint, equal), disjoint per-device strides, the
+  winner from the right stride, exact per-device exhaustion, cancellation reaching every device,
+  bursts and sweeps split over devices, subset masks.
+* tests/sweep_split_worker.py (G = 2, 4, 8): BASELINE configs[2] at full size -- the 2^36 sweep of the
+  fixture root split over G devices, bit-exact against tests/golden/sweep_2p36.json, the devices'
   nonce counters adding up to exactly 2^36.
-* tests/overshoot_worker.py (G = 8): first-found cancellation -- after the host accepts a winner the
-  other devices stop within a bounded time (median under 0.5 ms, host-observed)."""
+* tests/overshoot_worker.py: first-found cancellation -- after the host accepts a winner the other
+  devices stop within a bounded time: p50 AND p99 of the host-observed span on CU partitions (4 and 8
+  devices), next to the nonces the losers' waves hashed after they knew (counted in the kernels).
+With two or more physical GPUs visible (and NANOPOW_VIRTUAL_DEVICES unset) the same workers also run
+over the physical GPUs: the 2^36 sweep, the overshoot bound and a 64-root burst.  On a one-GPU box
+those tests skip."""
+import functools
 import json
 import os
 import subprocess
@@ -20,9 +29,20 @@ from conftest import ROOT
 
 pytestmark = pytest.mark.gpu
 
+# First-found cancellation bounds on CU partitions (host-observed, npow_wait_info.stop_after_decide_us):
+# the kill's way to the waves (one poll, within an iteration of ~15 us), one or two more hashes, and the
+# losing worker's observation of its launch's end.  Measured on the MI355X: see DESIGN.md section 5.
+P50_BOUND_US = 300.0
+P99_BOUND_US = 1500.0
+
 
 def _child(script, env_extra, *args, timeout=110):
-    env = dict(os.environ, **env_extra)
+    env = dict(os.environ)
+    for k, v in env_extra.items():
+        if v is None:
+            env.pop(k, None)
+        else:
+            env[k] = v
     p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", script), *args], env=env,
                        capture_output=True, text=True, timeout=timeout)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
@@ -31,9 +51,29 @@ def _child(script, env_extra, *args, timeout=110):
     return out
 
 
+@functools.lru_cache(maxsize=1)
+def physical_gpus() -> int:
+    """HIP devices the engine opens without NANOPOW_VIRTUAL_DEVICES (a child process: npow_init is
+    process-wide)."""
+    code = ("import sys; sys.path.insert(0, 'nano-dpow_amd'); from nanopow import _lib; "
+            "print(_lib.Engine().n_devices)")
+    env = {k: v for k, v in os.environ.items() if k != "NANOPOW_VIRTUAL_DEVICES"}
+    p = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stderr[-2000:]
+    return int(p.stdout.strip().splitlines()[-1])
+
+
+def _check_partitions(out, g):
+    parts = out["partitions"]
+    assert len(parts) == g
+    if g > 1:
+        assert all(first >= 0 for _hip, first, _cus in parts), parts  # CU partitions, not time-sharing
+
+
 def test_four_logical_devices():
     out = _child("multidev_worker.py", {"NANOPOW_VIRTUAL_DEVICES": "4"})
     assert out["ok"] and out["devices"] == 4
+    _check_partitions(out, 4)
 
 
 @pytest.mark.parametrize("g", [2, 4, 8])
@@ -41,9 +81,59 @@ def test_sweep_2p36_split_over_devices(g):
     out = _child("sweep_split_worker.py", {"NANOPOW_VIRTUAL_DEVICES": str(g)})
     assert out["ok"] and out["devices"] == g and out["hits"] == 126
     assert sum(out["nonces_per_device"]) == 1 << 36
+    _check_partitions(out, g)
 
 
-def test_first_win_overshoot_bound_8_devices():
-    out = _child("overshoot_worker.py", {"NANOPOW_VIRTUAL_DEVICES": "8"}, "200", "receive")
+@pytest.mark.parametrize("g", [4, 8])
+def test_first_win_overshoot_bound_cu_partitions(g):
+    out = _child("overshoot_worker.py", {"NANOPOW_VIRTUAL_DEVICES": str(g)}, "200", "receive")
+    assert out["ok"] and out["devices"] == g and out["kills_relayed"] > 0
+    assert all(first >= 0 for _hip, first, _cus in out["partitions"]), out["partitions"]
+    s = out["stop_after_decide_us"]
+    assert s["p50"] < P50_BOUND_US and s["p99"] < P99_BOUND_US, out
+    # the losers' waves hashed something after they knew (at least one hash of a workgroup), and no more
+    # than a few hashes of every workgroup of every losing device (2 x 512 lanes x 4 workgroups per CU)
+    late = out["late_nonces_losers"]
+    assert 0 < late["p50"] <= 2 * 512 * 4 * 256, out
+
+
+def test_first_win_overshoot_time_shared_8_devices():
+    """The rounds-1-3 rehearsal (8 logical devices time-sharing the whole GPU), kept for comparison: its
+    tail is the time-sharing (a losing launch waits for CUs behind the other devices' launches)."""
+    out = _child("overshoot_worker.py", {"NANOPOW_VIRTUAL_DEVICES": "8", "NANOPOW_VIRTUAL_PARTITION": "share"},
+                 "200", "receive")
     assert out["ok"] and out["devices"] == 8 and out["kills_relayed"] > 0
+    assert all(first < 0 for _hip, first, _cus in out["partitions"])
     assert out["stop_after_decide_us"]["p50"] < 500.0, out
+
+
+def _need_physical():
+    if os.environ.get("NANOPOW_VIRTUAL_DEVICES"):
+        pytest.skip("NANOPOW_VIRTUAL_DEVICES is set: the physical-GPU tests run without it")
+    n = physical_gpus()
+    if n < 2:
+        pytest.skip(f"{n} physical GPU visible: the physical multi-GPU tests need 2 or more "
+                    "(the CU-partition tests above stand in for them)")
+    return n
+
+
+def test_physical_gpus_sweep_2p36():
+    n = _need_physical()
+    out = _child("sweep_split_worker.py", {"NANOPOW_VIRTUAL_DEVICES": None, "EXPECT_DEVICES": str(n)})
+    assert out["ok"] and out["devices"] == n and out["hits"] == 126
+    assert sum(out["nonces_per_device"]) == 1 << 36
+    assert len({hip for hip, _first, _cus in out["partitions"]}) == n  # one logical device per GPU
+
+
+def test_physical_gpus_overshoot_bound():
+    n = _need_physical()
+    out = _child("overshoot_worker.py", {"NANOPOW_VIRTUAL_DEVICES": None}, "200", "receive")
+    assert out["ok"] and out["devices"] == n and out["kills_relayed"] > 0
+    s = out["stop_after_decide_us"]
+    assert s["p50"] < P50_BOUND_US and s["p99"] < P99_BOUND_US, out
+
+
+def test_physical_gpus_burst_64():
+    n = _need_physical()
+    out = _child("multidev_worker.py", {"NANOPOW_VIRTUAL_DEVICES": None, "EXPECT_DEVICES": str(n)}, "burst")
+    assert out["ok"] and out["devices"] == n

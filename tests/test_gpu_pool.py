@@ -298,3 +298,22 @@ def test_sweep_and_values_are_not_starved_by_endless_searches(gpu_engine):
         c.set()
     for t in ts:
         assert t.wait(30).status == _lib.NPOW_CANCELLED
+
+
+def test_cpu_workers_beside_the_gpu():
+    """--cpu-threads (nano-work-server.exe @1681064): 4 CPU worker threads as one more device of the pool,
+    beside the GPU(s), in a process of its own (tests/cpu_workers_worker.py): CPU-only searches decided by
+    the CPU device and re-validated by hashlib, exact bounded exhaustion, the first hit of a single-claim
+    range, a hit only the CPU stride holds, GPU + CPU searches at receive difficulty, cancellation, and
+    sweeps / values refused on the CPU device."""
+    import json
+    import os
+    import subprocess
+    import sys
+    from conftest import ROOT
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "cpu_workers_worker.py")],
+                       capture_output=True, text=True, timeout=110)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    out = json.loads(p.stdout.strip().splitlines()[-1])
+    print(json.dumps(out))
+    assert out["ok"] and out["mixed_receive"]["cpu_nonces"] > 0

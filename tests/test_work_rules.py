@@ -55,9 +55,64 @@ def test_gpu_spec_and_cli():
     assert parse_args([]).listen == "127.0.0.1:7000"
 
 
-def test_cpu_threads_rejected():
+def test_cpu_threads_out_of_range_rejected():
     from nanopow.__main__ import main
-    assert main(["--cpu-threads", "4"]) == 2
+    assert main(["--cpu-threads", "-1"]) == 2
+    assert main(["--cpu-threads", "5000"]) == 2
+
+
+def test_cli_with_cpu_threads_serves_the_transcript(monkeypatch):
+    """`python -m nanopow --cpu-threads 2 --gpu 0:0 -l 127.0.0.1:P` starts (the reference's
+    launch pattern, client/README.md:31, plus nano-work-server.exe @1681064 `cpu_threads`) and serves
+    the WorkHandler transcript.  The engine is the oracle stand-in with 2 logical devices, the second
+    playing the CPU workers' device: the CLI must ask the engine for 2 CPU threads and search over GPU 0
+    and the CPU device (mask 0b11).  On the GPU the real CPU workers are tested in
+    tests/test_gpu_pool.py::test_cpu_workers_beside_the_gpu."""
+    import json
+    import threading
+    import urllib.request
+
+    import oracle
+    from conftest import load_golden
+    from fake_engine import OracleEngine
+    from nanopow import _lib
+    from nanopow.__main__ import build, parse_args
+
+    seen = {}
+
+    def fake_engine(cpu_threads=0):
+        seen["cpu_threads"] = cpu_threads
+        e = OracleEngine(chunk=1 << 12, n_devices=2)
+        e.cpu_device, e.gpu_mask = 1, 0b01
+        return e
+    monkeypatch.setattr(_lib, "engine", fake_engine)
+    srv = build(parse_args(["--cpu-threads", "2", "--gpu", "0:0", "-l", "127.0.0.1:0", "--max-active", "1"]))
+    assert not isinstance(srv, int)
+    assert seen["cpu_threads"] == 2 and srv.work_server.device_mask == 0b11
+    srv.start()
+    try:
+        def post(obj):
+            req = urllib.request.Request(f"http://{srv.address}", data=json.dumps(obj).encode(), method="POST")
+            with urllib.request.urlopen(req, timeout=30) as r:
+                return json.loads(r.read())
+        reqs = load_golden("workhandler_transcript.json")["requests"]
+        assert post(reqs[0])["error"] == "Unknown command"
+        g = dict(reqs[1], difficulty="fffff00000000000")
+        r1 = post(g)
+        assert oracle.work_value_hashlib(bytes.fromhex(g["hash"]), int(r1["work"], 16)) >= 0xfffff00000000000
+        hold = dict(reqs[2], difficulty="ffffffffffffffff")
+        box = {}
+        th = threading.Thread(target=lambda: box.setdefault("r", post(hold)))
+        th.start()
+        import time
+        time.sleep(0.3)
+        assert post(reqs[3]) == {}
+        th.join(10)
+        assert box["r"] == {"error": "Cancelled"}
+    finally:
+        srv.stop()
+    # a --gpu index past the GPUs (the CPU device is not a GPU) is refused
+    assert build(parse_args(["--cpu-threads", "2", "--gpu", "0:1", "-l", "127.0.0.1:0"])) == 2
 
 
 def test_gpu_threads_is_a_lower_bound_on_the_launch():

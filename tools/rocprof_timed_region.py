@@ -33,6 +33,23 @@ def main():
           f"-> agreement {abs(avg - ev) / ev * 100:.2f} %")
     print(f"bench under the profiler: value {b['value']} Gnonce/s, kernel_gnps {b['roofline']['kernel_gnps']}, "
           f"frac {b['roofline']['frac']}, in-kernel clock {b['sclk_mhz']['mean']} MHz")
+    # round 4: the roofline fraction recomputed from this profile alone (bench.py names this file in
+    # roofline.profile when its build_sha16 equals the bench's own)
+    ro = b["roofline"]
+    npl = ro["nonces_per_launch"]
+    ex = ro.get("executed_ops_per_nonce", 2086)
+    peak = ro["peak"]
+    frac = npl * ex / (avg * 1e-3) / 1e12 / peak
+    print()
+    if "build_sha16" in b:
+        print(f"build_sha16 {b['build_sha16']}")
+    print(f"nonces_per_launch {npl}")
+    print(f"executed_ops_per_nonce {ex}")
+    print(f"frac_executed_from_profile {frac:.4f}")
+    print(f"  = {npl} nonces per launch x {ex} int32 ops / {avg:.4f} ms (the timed dispatches' rocprofv3 average) "
+          f"/ {peak} Tops/s = {npl * ex / (avg * 1e-3) / 1e12:.3f} Tops/s / {peak}")
+    if "frac_algorithmic" in ro:
+        print(f"frac_algorithmic_from_profile {npl * 2232 / (avg * 1e-3) / 1e12 / peak:.4f} (2,232 ops per nonce)")
 
 
 if __name__ == "__main__":
