@@ -64,3 +64,17 @@ def test_device_drop_under_sanitizers(binary):
     else:
         env.update(TSAN_OPTIONS="suppressions=tools/tsan.supp:halt_on_error=1")
     _run(binary, env)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("binary", ["abi_asan_driver", "abi_tsan_driver"])
+def test_cpu_workers_under_sanitizers(binary):
+    """The pool's CPU workers (npow_cpu.cpp, --cpu-threads) under ASan / TSan: 2 CPU threads as one more
+    device, every search, ticket (cancelled ones too) and bounded range over the GPU and the CPU device
+    (DRIVER_MASK=0)."""
+    env = {"DRIVER_CPU_THREADS": "2", "DRIVER_MASK": "0"}
+    if binary == "abi_asan_driver":
+        env.update(ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", LSAN_OPTIONS="suppressions=tools/lsan.supp")
+    else:
+        env.update(TSAN_OPTIONS="suppressions=tools/tsan.supp:halt_on_error=1")
+    _run(binary, env)

@@ -115,6 +115,15 @@ static void sweeps(int tid, int n) {
 
 int main() {
   int n_dev = 0;
+  // DRIVER_CPU_THREADS=N: the pool's CPU workers (--cpu-threads) as one more device; with DRIVER_MASK=0 every
+  // search, ticket and bounded range also runs on them
+  if (const char* c = std::getenv("DRIVER_CPU_THREADS")) {
+    const int rc0 = npow_config_cpu_threads((uint32_t)std::atoi(c));
+    if (rc0 != NPOW_OK) {
+      std::fprintf(stderr, "npow_config_cpu_threads rc %d: %s\n", rc0, npow_last_error());
+      return 2;
+    }
+  }
   int rc = npow_init(&n_dev);
   if (rc != NPOW_OK || n_dev < 1) {
     std::fprintf(stderr, "npow_init rc %d devices %d: %s\n", rc, n_dev, npow_last_error());
