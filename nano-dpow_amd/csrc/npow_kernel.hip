@@ -355,7 +355,7 @@ __device__ __forceinline__ void clk_end_ls2(const PoolTable* tab, PoolMailbox* m
 //    budget) files a request in LDS, s_stop[segment % 3] = min((it + 1) << 2 | kind) with kind 0 =
 //    end the launch, 1-3 = leave the entry (why: see the loop), drained before the iteration's closing s_barrier; every
 //    wave reads the word at the top of an iteration, so all waves see the same set of requests and
-//    leave together, one hash after the request (~16 us);
+//    leave together, before the next hash (round 4; one hash after it, ~16 us, until round 3);
 //  * leaving an entry: wave 0 picks the next entry and broadcasts it through LDS (one
 //    __syncthreads); each entry segment has its own request word (3 rotate: the word of segment
 //    s + 1 is reset at the end of segment s, after its last reader).
@@ -664,6 +664,16 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       const uint32_t verdict = __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const uint64_t dead = __hip_atomic_load(dead_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
+      // The verdict holds every request filed after the previous hashes: each was drained before the
+      // s_barrier closing its iteration, which every wave passed before this read.  So all waves see the same
+      // set here and leave together, before this hash (round 4; rounds 2-3 acted on it after the hash: one
+      // more hash per stop).  A request of this iteration from a wave already past its hash (value > it) is
+      // left for the next read, which every wave makes.
+      const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(verdict);
+      if (v != ~0u && (v >> 2) <= it) {
+        end = (v & 3u) == 0;
+        break;
+      }
       const uint32_t it0 = it;  // the poll phase
       const uint64_t thr = c.threshold, gen = c.gen;
       const uint64_t value = npow_asm_work_value_lockstep_ld(nonce, c.up);
@@ -711,14 +721,6 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       }
       nonce += step;
       b += c.K;
-      // The verdict as read before this hash holds every request filed before it: each one was
-      // drained before the s_barrier below, which every wave passes before its next read.  So
-      // all waves see the same set and leave together, one hash after the request.
-      const uint32_t v = (uint32_t)__builtin_amdgcn_readfirstlane(verdict);
-      if (v != ~0u) {
-        end = (v & 3u) == 0;
-        break;
-      }
       __builtin_amdgcn_s_barrier();
     }
     // the workgroup's count, added by wave 0 before it leaves the entry (early finish, ls2_leave):
@@ -730,15 +732,16 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
 #pragma unroll
       for (int m = kLsWaves / 2; m >= 1; m >>= 1) sum += __shfl_xor(sum, m);
       // device-side overshoot: the workgroup's hashes of this entry that started after one of its waves knew
-      // the entry was over -- a request filed after hash i ends the loop after hash i + 1, so 2 such hashes per
-      // wave when the dead word was already up before hash i (kind 1), 1 when hash i itself revealed it (kind 2).
-      // Every wave of the workgroup leaves at the same iteration; capped by the workgroup's count.
+      // the entry was over -- a request filed after hash i ends the loop before hash i + 1, so one such hash
+      // per wave when the dead word was already up before hash i (kind 1; its value is read after the hash
+      // that its load's latency hides behind), none when hash i itself revealed it (kind 2: a win, a kill read
+      // by a poll).  Every wave of the workgroup leaves at the same iteration; capped by the workgroup's count.
       // (read back from LDS after the barrier above rather than kept in a register through the loop: one more
       // value live across the loop spilled to scratch)
       const uint32_t v = __builtin_amdgcn_readfirstlane(
           __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      const uint32_t kind = v != ~0u && (v >> 2) + 1u == it ? (v & 3u) : 0u;  // the loop ended on this request
-      uint32_t late_n = kind == 1u ? 2u * 64u * kLsWaves : (kind == 2u ? 64u * kLsWaves : 0u);
+      const uint32_t kind = v != ~0u && (v >> 2) == it ? (v & 3u) : 0u;  // the loop ended on this request
+      uint32_t late_n = kind == 1u ? 64u * kLsWaves : 0u;
       late_n = late_n < sum ? late_n : sum;
       ls2_leave_wave(st, mb, c.slot, c.gen, sum, late_n, counted);
     }

@@ -51,7 +51,7 @@ def main(n_search, which):
     st = [eng.stats(d) for d in range(G)]
     kills = sum(x.kills_relayed for x in st)
     res = {"ok": True, "devices": G, "threshold": which, "searches": n_search,
-           "partition": [[x.hip_device, x.cu_first, x.cus] for x in st],
+           "partitions": [[x.hip_device, x.cu_first, x.cus] for x in st],
            "stop_after_decide_us": {"p50": round(pct(spans, 50), 1), "p99": round(pct(spans, 99), 1),
                                     "max": round(max(spans), 1)},
            "overshoot_nonces": {"p50": pct(over, 50), "p99": pct(over, 99),
