@@ -1431,9 +1431,18 @@ def main_inprocess(eng, args) -> int:
         line["sysfs_sclk_mhz"] = clk
     line["timed_overshoot"] = overshoot_summary([r[2] for r in recs], [r[3] for r in recs], [r[1] for r in recs])
     if os.environ.get("NANOPOW_VIRTUAL_DEVICES"):
-        line["virtual_devices_note"] = (f"NANOPOW_VIRTUAL_DEVICES: the {n} devices are logical ones time-sharing one "
-                                        "GPU; their launches overlap, so per-device kernel times, the roofline and "
-                                        "the overshoot spans are not those of separate GPUs (a rehearsal of the path)")
+        parts = [[k.hip_device, k.cu_first, k.cus] for k in ks]
+        if all(p[1] >= 0 for p in parts):
+            line["virtual_devices_note"] = (
+                f"NANOPOW_VIRTUAL_DEVICES: the {n} devices are CU partitions of one GPU (CU-masked streams, "
+                f"[hip device, first CU, CUs] = {parts}): every launch runs from its start on CUs of its own, as on "
+                "separate GPUs, but they share one card's clock and power cap and HBM; kernel_gnps_per_gpu is per "
+                "partition, the roofline is priced for a whole GPU (a rehearsal of the path)")
+        else:
+            line["virtual_devices_note"] = (
+                f"NANOPOW_VIRTUAL_DEVICES with NANOPOW_VIRTUAL_PARTITION=share: the {n} devices time-share one GPU; "
+                "their launches overlap, so per-device kernel times, the roofline and the overshoot spans are not "
+                "those of separate GPUs (a rehearsal of the path)")
     line["early_finishes"] = sum(k.early_finishes for k in ks)
     line["kills_relayed"] = sum(k.kills_relayed for k in ks)
     if args.node_searches:

@@ -819,6 +819,12 @@ int Worker::retire() {
       if (sl.job && sl.job->max_per_dev && !sl.win_seen && sl.stop_us == 0)
         for (size_t i = 0; i < m; ++i) sl.unread += sl.inflight[i].count;
       sl.inflight.erase(sl.inflight.begin(), sl.inflight.begin() + (ptrdiff_t)m);
+      // a decided job's last launch on this device has completed: the device hashes nothing more of it, so
+      // its stop time is now (npow_wait_info), not when the done counts' read-back lands
+      if (m > 0 && sl.inflight.empty() && sl.state == SlotState::kDraining && sl.job && sl.job->decided.load()) {
+        std::lock_guard<std::mutex> g(g_pool.mu);
+        if (sl.job->t_stop[sl.k] == 0) sl.job->t_stop[sl.k] = now_us();
+      }
     }
     if (g_trace_lat)
       for (Slot& sl : slots_)
@@ -1204,10 +1210,17 @@ int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* va
     info->late_nonces_losers = dev_late;
     info->late_nonces_winner = j->winner_k >= 0 ? j->late[(size_t)j->winner_k] : 0;
   }
-  if (g_trace_lat)
-    fprintf(stderr, "nanopow-lat adopt %.1f launch %.1f win %.1f kend %.1f finish %.1f return %.1f\n",
-            j->t_adopt - j->t_submit, j->t_launch - j->t_submit, j->t_win - j->t_submit, j->t_kend - j->t_submit,
-            j->t_finish - j->t_submit, now_us() - j->t_submit);
+  if (g_trace_lat) {
+    fprintf(stderr, "nanopow-lat adopt %.1f launch %.1f win %.1f kend %.1f finish %.1f return %.1f", j->t_adopt - j->t_submit,
+            j->t_launch - j->t_submit, j->t_win - j->t_submit, j->t_kend - j->t_submit, j->t_finish - j->t_submit,
+            now_us() - j->t_submit);
+    if (j->devs.size() > 1 && j->t_decide > 0) {  // the devices' stop times after the decision
+      fprintf(stderr, " decide %.1f stops", j->t_decide - j->t_submit);
+      for (size_t k = 0; k < j->devs.size(); ++k)
+        fprintf(stderr, " %s%.1f", (int)k == j->winner_k ? "*" : "", j->t_stop[k] > 0 ? j->t_stop[k] - j->t_decide : -1.0);
+    }
+    fprintf(stderr, "\n");
+  }
   const int st = j->status;
   g_pool.tickets.erase(ticket);
   if (st == NPOW_OK) {
