@@ -212,6 +212,21 @@ def pct(xs, p):
 CHECK_THR = 0xfffff00000000000  # cpu_baseline: hits kept at this lower threshold for the parity cross-check
 
 
+def search_to_result(eng, root: bytes, thr: int, start: int, mask: int):
+    """One search as the work server serves it (round 4): submit, the outcome at the decision
+    (npow_wait_result -- what the client is answered with), then the ticket collected (npow_wait_info:
+    every device stopped, nonces_done complete).  Returns (seconds to the result, seconds to the
+    collection, info).  Time-to-work is the first."""
+    t = time.perf_counter()
+    tk = eng.submit(root, thr, start=start, device_mask=mask)
+    r = tk.wait_result()
+    t_res = time.perf_counter() - t
+    if r is None or r.status != 0:
+        raise RuntimeError(f"search returned status {None if r is None else r.status}")
+    info = tk.wait_info()
+    return t_res, time.perf_counter() - t, info
+
+
 def _hashlib_scan(job):
     """The reference CPU path (hashlib.blake2b(digest_size=8), dpow_server.py:130 rule value >= d)
     over nonces [start, start + count) of one root; returns (hits >= CHECK_THR, seconds)."""
@@ -412,12 +427,13 @@ def node_time_to_work(eng, dev: int, rank: int, world: int, dist, m: int, thr: i
             idx = 3_000_000 + i
             t = time.perf_counter()
             try:
-                r = eng.search(bench_root(idx), thr, start=(bench_start(idx) + rank * spacing) & ((1 << 64) - 1),
-                               device_mask=1 << dev, cancel=tok)
+                tk = eng.submit(bench_root(idx), thr, start=(bench_start(idx) + rank * spacing) & ((1 << 64) - 1),
+                                device_mask=1 << dev, cancel=tok)
+                r = tk.wait_result()  # the outcome at the decision: the winner raises the word at once
                 dt = time.perf_counter() - t
                 if r.status == 0 and tok is not None:
                     tok.set()
-                recs.append((dt, r.status, r.nonces_done))
+                recs.append((dt, r.status, tk.wait().nonces_done))
             except Exception:  # keep the collectives aligned; reported as a failed search
                 recs.append((None, -1, 0))
         dist.barrier()
@@ -1124,13 +1140,9 @@ def fixed_overhead(eng, mask: int, rate: float, n: int = 300):
     first hash wins, and 8,192 win atomics on one word serialise for ~0.15 ms.)"""
     res, ts = [], []
     for i in range(n):
-        t = time.perf_counter()
-        r = eng.search(bench_root(40_000_000 + i), 0xfffffe0000000000, start=bench_start(i), device_mask=mask)
-        dt = time.perf_counter() - t
-        if r.status != 0:
-            raise RuntimeError(f"overhead search {i} returned status {r.status}")
+        dt, _t_all, info = search_to_result(eng, bench_root(40_000_000 + i), 0xfffffe0000000000, bench_start(i), mask)
         ts.append(dt)
-        res.append(dt - r.nonces_done / rate)
+        res.append(dt - info.nonces_done / rate)
     return {"p50": round(pct(res, 50) * 1e3, 4), "mean": round(statistics.mean(res) * 1e3, 4), "n": n,
             "receive_p50_ms": round(pct(ts, 50) * 1e3, 4),
             "how": "receive-difficulty searches (fffffe00...) one at a time: wall time - nonces_done / kernel rate"}
@@ -1141,15 +1153,13 @@ def latency_sample(eng, dev: int, n: int, rate_gnps=None):
     fffffff8 through the C ABI, one at a time, after the timed region (not part of value), with the
     decomposition of its p50 / mean: the sample's own nonce counts against the exponential law's
     (E = 2^29, median ln2 * 2^29), the fixed per-search overhead, and the kernel rate."""
-    ttw, nn = [], []
+    ttw, nn, coll = [], [], []
     t0 = time.perf_counter()
     for i in range(n):
-        t = time.perf_counter()
-        r = eng.search(bench_root(i), SEND, start=bench_start(i), device_mask=1 << dev)
-        ttw.append(time.perf_counter() - t)
-        if r.status != 0:
-            raise RuntimeError(f"latency search {i} returned status {r.status}")
-        nn.append(r.nonces_done)
+        t_res, t_all, info = search_to_result(eng, bench_root(i), SEND, bench_start(i), 1 << dev)
+        ttw.append(t_res)
+        coll.append(t_all)
+        nn.append(info.nonces_done)
     wall = time.perf_counter() - t0
     E = float(1 << 29)
     ln2 = 0.6931471805599453
@@ -1160,6 +1170,9 @@ def latency_sample(eng, dev: int, n: int, rate_gnps=None):
     oh = over["p50"] * 1e-3
     out = {"p50": round(pct(ttw, 50) * 1e3, 3), "p99": round(pct(ttw, 99) * 1e3, 3),
            "mean": round(statistics.mean(ttw) * 1e3, 3), "n": n, "gnps": round(sum(nn) / wall / 1e9, 4),
+           "collected_p50": round(pct(coll, 50) * 1e3, 3),
+           "what": "submit -> npow_wait_result (the winner accepted: what a client is answered with); "
+                   "collected_p50: -> npow_wait_info (the device stopped, nonces_done complete)",
            "roots": f"R_0..R_{n - 1}",
            "nonces_per_search": {
                "mean_over_2p29": round(mean_n / E, 4), "se_over_2p29": round(se_n / E, 4),
@@ -1246,23 +1259,24 @@ def inprocess_node_ttw(eng, n_dev: int, m: int, thr: int = SEND):
     into disjoint per-GPU strides, first found cancels the others): p50/p99 time-to-work at N GPUs
     and each search's overshoot (npow_wait_info)."""
     mask = (1 << n_dev) - 1
-    ttw, spans, over, done, decide = [], [], [], [], []
+    ttw, spans, over, done, decide, fin, late = [], [], [], [], [], [], []
     t0 = time.perf_counter()
     for i in range(m):
         idx = 3_000_000 + i
-        t = time.perf_counter()
-        info = eng.submit(bench_root(idx), thr, start=bench_start(idx), device_mask=mask).wait_info()
-        ttw.append(time.perf_counter() - t)
-        if info.status != 0:
-            raise RuntimeError(f"node search {idx} returned status {info.status}")
+        t_res, t_all, info = search_to_result(eng, bench_root(idx), thr, bench_start(idx), mask)
+        ttw.append(t_res)
+        fin.append(t_all)
         spans.append(info.stop_after_decide_us)
         over.append(info.overshoot_nonces)
         done.append(info.nonces_done)
         decide.append(info.decide_us)
+        late.append(info.late_nonces_losers)
     wall = time.perf_counter() - t0
     return {"p50": round(pct(ttw, 50) * 1e3, 3), "p99": round(pct(ttw, 99) * 1e3, 3),
             "mean": round(statistics.mean(ttw) * 1e3, 3), "n": m, "node_gnps": round(sum(done) / wall / 1e9, 4),
             "decide_p50_ms": round(pct(decide, 50) / 1e3, 3),
+            "collected_p50_ms": round(pct(fin, 50) * 1e3, 3),
+            "late_nonces_losers_p50": int(pct(late, 50)),
             "nonces_per_search": round(statistics.mean(done)),
             **overshoot_summary(spans, over, done),
             "note": f"one root at a time searched by all {n_dev} GPUs of the process on disjoint strides "
@@ -1280,10 +1294,9 @@ def workload_receive(eng, args, rank, world, dist):
     # GPU through the C ABI
     gpu = []
     for i in range(args.steps):
-        t = time.perf_counter()
-        r = eng.search(bench_root(20_000_000 + i), recv, start=bench_start(i), device_mask=0)
-        gpu.append(time.perf_counter() - t)
-        assert r.status == 0 and r.value >= recv
+        dt, _t_all, info = search_to_result(eng, bench_root(20_000_000 + i), recv, bench_start(i), 0)
+        gpu.append(dt)
+        assert info.status == 0 and info.value >= recv
     # GPU through the HTTP work server (what the DPoW client sees): one keep-alive connection, as
     # the client's aiohttp session, and a new connection per request
     http = _http_ttw(eng, min(args.steps, 300), thr=recv, base=21_000_000, device_mask=0)
@@ -1528,12 +1541,10 @@ def main() -> int:
         return main_inprocess(eng, args)
 
     def search(i):
-        t = time.perf_counter()
-        r = eng.search(bench_root(i), SEND, start=bench_start(i), device_mask=1 << dev)
-        dt = time.perf_counter() - t
-        if r.status != _lib.NPOW_OK:
-            raise RuntimeError(f"search {i} returned status {r.status}")
-        return dt, r.nonces_done
+        # time-to-work at the result (npow_wait_result), nonces after the ticket's collection; the timed
+        # region's wall time includes the collection (the next search starts after it)
+        t_res, _t_all, info = search_to_result(eng, bench_root(i), SEND, bench_start(i), 1 << dev)
+        return t_res, info.nonces_done
 
     timed_stats = []
 

@@ -54,7 +54,8 @@ extern "C" {
 /* ABI revision (npow_abi_version()).  3: npow_values runs the search kernels' stream;
  * npow_values_path, npow_wait_info, npow_device_stats_get_sized added;
  * npow_device_stats_get writes only the revision-2 prefix of npow_device_stats.
- * 4: npow_config_cpu_threads (CPU workers, --cpu-threads); npow_device_stats gains late_nonces,
+ * 4: npow_config_cpu_threads (CPU workers, --cpu-threads), npow_wait_result (the outcome at the decision);
+ * npow_device_stats gains late_nonces,
  * hip_device, cu_first; npow_search_info gains late_nonces_losers / late_nonces_winner (both structs
  * are written up to the size the caller passes, so revision-3 callers are unaffected). */
 #define NPOW_ABI_VERSION 4
@@ -207,6 +208,15 @@ int npow_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce_out, uint64_t
 /* npow_wait with the search's outcome and timeline in *info (info->size set by the caller; the
  * library writes at most that many bytes).  Returns as npow_wait. */
 int npow_wait_info(uint64_t ticket, int64_t timeout_us, npow_search_info* info);
+
+/* The search's outcome as soon as it is known (ABI 4): NPOW_OK with nonce / value once a winner has passed
+ * CPU re-validation, NPOW_CANCELLED once the cancellation is seen, NPOW_EXHAUSTED or an error when the search
+ * ends so, NPOW_PENDING on timeout.  Unlike npow_wait it does not wait for the other devices of a split
+ * search to stop, nor release the ticket: collect it with npow_wait / npow_wait_info afterwards (nonces_done
+ * is complete only there), and keep the cancel word valid until then.  The reference work server answers a
+ * work_generate as soon as its result validates (nano-work-server.exe @1669040); the JSON server here replies
+ * at this point and collects the ticket after the reply. */
+int npow_wait_result(uint64_t ticket, int64_t timeout_us, uint64_t* nonce_out, uint64_t* value_out);
 
 /* Cancel a ticket (same effect as raising its cancel word). */
 int npow_cancel(uint64_t ticket);

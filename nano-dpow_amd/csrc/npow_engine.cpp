@@ -596,6 +596,11 @@ int npow_wait_info(uint64_t ticket, int64_t timeout_us, npow_search_info* info) 
   return rc;
 } catch (...) { return guard_exception(); }
 
+int npow_wait_result(uint64_t ticket, int64_t timeout_us, uint64_t* nonce_out, uint64_t* value_out) try {
+  if (int rc = check_init()) return rc;
+  return pool_wait_result(ticket, timeout_us, nonce_out, value_out);
+} catch (...) { return guard_exception(); }
+
 int npow_cancel(uint64_t ticket) try {
   if (int rc = check_init()) return rc;
   return pool_cancel(ticket);

@@ -145,6 +145,7 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
 // info (may be null): the search's timeline and overshoot (npow_wait_info)
 int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done,
               npow_search_info* info = nullptr);
+int pool_wait_result(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value);
 int pool_cancel(uint64_t ticket);
 int pool_set_max_active(uint32_t n);
 void pool_counts(uint32_t* queued, uint32_t* active);

@@ -150,6 +150,7 @@ void decide_locked(Job& j, int status, uint64_t nonce, uint64_t value) {
   j.nonce = nonce;
   j.value = value;
   j.decided = true;
+  j.cv.notify_all();  // npow_wait_result returns at the decision
 }
 
 void admit_locked() {
@@ -1223,6 +1224,41 @@ int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* va
   }
   const int st = j->status;
   g_pool.tickets.erase(ticket);
+  if (st == NPOW_OK) {
+    if (nonce) *nonce = j->nonce;
+    if (value) *value = j->value;
+    return NPOW_OK;
+  }
+  if (st < 0) return fail(st, j->err.empty() ? std::string("work generation failed") : j->err);
+  return st;
+}
+
+// The search's outcome as soon as it is known (npow_wait_result): the winner accepted or the job cancelled,
+// while the other devices may still be stopping; the ticket stays valid for pool_wait.
+int pool_wait_result(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value) {
+  std::unique_lock<std::mutex> lk(g_pool.mu);
+  auto it = g_pool.tickets.find(ticket);
+  if (it == g_pool.tickets.end()) return fail(NPOW_ERR_BAD_ARGUMENT, "unknown ticket");
+  JobP j = it->second;
+  const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us < 0 ? 0 : timeout_us);
+  while (j->status == kPending && !j->finished) {
+    if (!j->admitted && j->cancel_seen()) {  // as pool_wait: a queued job's cancel word is polled here
+      j->cancel_req = true;
+      decide_locked(*j, NPOW_CANCELLED);
+      finish_locked(j);
+      break;
+    }
+    const auto now = std::chrono::steady_clock::now();
+    if (timeout_us >= 0 && now >= deadline) return NPOW_PENDING;
+    if (j->admitted && timeout_us < 0) {
+      j->cv.wait(lk);
+    } else {
+      auto wake = j->admitted ? deadline : now + std::chrono::microseconds(2000);
+      if (timeout_us >= 0) wake = std::min(wake, deadline);
+      j->cv.wait_until(lk, wake);
+    }
+  }
+  const int st = j->status;
   if (st == NPOW_OK) {
     if (nonce) *nonce = j->nonce;
     if (value) *value = j->value;

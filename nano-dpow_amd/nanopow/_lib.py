@@ -45,7 +45,7 @@ EXPORTED_SYMBOLS = (
     "npow_device_stats_get", "npow_device_stats_reset", "npow_version",
     "npow_submit", "npow_wait", "npow_cancel", "npow_pool_config", "npow_pool_status",
     "npow_set_pool_tuning", "npow_values_path", "npow_wait_info", "npow_device_stats_get_sized",
-    "npow_abi_version", "npow_config_cpu_threads",
+    "npow_abi_version", "npow_config_cpu_threads", "npow_wait_result",
 )
 
 
@@ -185,6 +185,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         if hasattr(lib, "npow_config_cpu_threads"):  # ABI 4
             lib.npow_config_cpu_threads.argtypes = [u32]
             lib.npow_config_cpu_threads.restype = ctypes.c_int
+            lib.npow_wait_result.argtypes = [u64, ctypes.c_int64, pu64, pu64]
+            lib.npow_wait_result.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -251,6 +253,22 @@ class Ticket:
         self.result = (SearchResult(rc, nonce.value, value.value, done.value) if rc == NPOW_OK
                        else SearchResult(rc, None, None, done.value))
         return self.result
+
+    def wait_result(self, timeout: Optional[float] = None) -> Optional[SearchResult]:
+        """The search's outcome as soon as it is known (npow_wait_result: the winner accepted, the cancellation
+        seen), before the other devices of a split search have stopped; None if still running after `timeout`
+        seconds.  nonces_done is 0 here: wait() or wait_info() must still collect the ticket."""
+        if self.result is not None:
+            return self.result
+        lib = self.engine.lib
+        nonce, value = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        us = -1 if timeout is None else max(0, int(timeout * 1e6))
+        rc = lib.npow_wait_result(self.ticket, us, ctypes.byref(nonce), ctypes.byref(value))
+        if rc == NPOW_PENDING:
+            return None
+        _check(rc, lib, ok=(NPOW_OK, NPOW_CANCELLED, NPOW_EXHAUSTED))
+        return (SearchResult(rc, nonce.value, value.value, 0) if rc == NPOW_OK
+                else SearchResult(rc, None, None, 0))
 
     def wait_info(self, timeout: Optional[float] = None) -> Optional[SearchInfo]:
         """wait() with the search's timeline (npow_wait_info): winner device, host times of the

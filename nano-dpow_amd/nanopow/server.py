@@ -36,6 +36,7 @@ from __future__ import annotations
 import json
 import logging
 import os
+import queue
 import random
 import socket
 import socketserver
@@ -111,6 +112,9 @@ class WorkServer:
         self._queue: List[Job] = []
         self._inflight: List[Job] = []
         self._running = False
+        # tickets answered at their decision (npow_wait_result) and collected after the reply
+        self._reap_q: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._reaper: Optional[threading.Thread] = None
 
     # -- lifecycle ---------------------------------------------------------------------
     def start(self) -> "WorkServer":
@@ -132,6 +136,29 @@ class WorkServer:
         with self._lock:
             while self._inflight and time.time() < deadline:
                 self._lock.wait(0.1)
+            reaper, self._reaper = self._reaper, None
+        if reaper is not None:
+            self._reap_q.put(None)
+            reaper.join(10)
+
+    def _reap(self, ticket) -> None:
+        """Collect a ticket whose reply has gone out (its other devices may still be stopping): one
+        thread, started on first use, waits for each in turn (npow_wait)."""
+        with self._lock:
+            if self._reaper is None:
+                self._reaper = threading.Thread(target=self._reap_loop, name="nanopow-reaper", daemon=True)
+                self._reaper.start()
+        self._reap_q.put(ticket)
+
+    def _reap_loop(self) -> None:
+        while True:
+            t = self._reap_q.get()
+            if t is None:
+                return
+            try:
+                t.wait()
+            except Exception as e:  # the reply is out; only log
+                log.error("collecting a finished search: %s", e)
 
     # -- dispatch ----------------------------------------------------------------------
     def handle_body(self, raw: bytes) -> Dict[str, Any]:
@@ -274,7 +301,14 @@ class WorkServer:
 
     def _collect(self, job: Job) -> Dict[str, Any]:
         try:
-            res = job.ticket.wait()
+            t = job.ticket
+            early = hasattr(t, "wait_result")
+            # the reply as soon as the outcome is known (the reference answers when its result validates,
+            # nano-work-server.exe @1669040), before a split search's other devices have stopped; the
+            # ticket is collected after the reply (_reap)
+            res = t.wait_result() if early else t.wait()
+            if early:
+                self._reap(t)
             if res is not None and res.status == NPOW_OK:
                 log.info("Generated for %s in %.0fms for difficulty %016x", job.root.hex().upper(),
                          (time.perf_counter() - job.t_started) * 1000.0, job.threshold)

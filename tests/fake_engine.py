@@ -32,13 +32,16 @@ class _Ticket:
     def wait(self, timeout=None):
         return self._res if self._ev.wait(timeout) else None
 
+    def wait_result(self, timeout=None):  # the engine's npow_wait_result; here the outcome is the final result
+        return self.wait(timeout)
+
     def wait_info(self, timeout=None):
         if not self._ev.wait(timeout):
             return None
         r, info = self._res, self._info
         return info or SimpleNamespace(status=r.status, nonce=r.nonce, value=r.value, nonces_done=r.nonces_done,
                                        winner_device=0, n_devices=1, decide_us=0.0, finish_us=0.0,
-                                       stop_after_decide_us=0.0, overshoot_nonces=0)
+                                       stop_after_decide_us=0.0, overshoot_nonces=0, late_nonces_losers=0, late_nonces_winner=0)
 
 
 class OracleEngine:
@@ -104,7 +107,7 @@ class OracleEngine:
         info = SimpleNamespace(status=NPOW_OK, nonce=win.nonce, value=win.value, nonces_done=done,
                                winner_device=devs[k], n_devices=G, decide_us=(td - t0) * 1e6,
                                finish_us=(max(te for _, te in out) - t0) * 1e6,
-                               stop_after_decide_us=max(spans, default=0.0), overshoot_nonces=0)
+                               stop_after_decide_us=max(spans, default=0.0), overshoot_nonces=0, late_nonces_losers=0, late_nonces_winner=0)
         return res, info
 
     def work_value(self, root, nonce):

@@ -11,6 +11,7 @@ import os
 import random
 import statistics
 import sys
+import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
@@ -33,11 +34,15 @@ def main(n_search, which):
     G = eng.n_devices
     thr = THRESHOLDS[which]
     rng = random.Random(11)
-    spans, over, done, ttw, winners, late_l, late_w = [], [], [], [], [], [], []
+    spans, over, done, ttw, winners, late_l, late_w, res_ms = [], [], [], [], [], [], [], []
     for i in range(n_search):
         root = bytes(rng.getrandbits(8) for _ in range(32))
+        t0 = time.perf_counter()
         t = eng.submit(root, thr, start=rng.getrandbits(64), device_mask=0)
+        r = t.wait_result(120)  # the outcome at the decision (what a client is answered with)
+        res_ms.append((time.perf_counter() - t0) * 1e3)
         info = t.wait_info(120)
+        assert r.status == info.status and r.nonce == info.nonce
         assert info is not None and info.status == _lib.NPOW_OK, info
         assert oracle.work_value_hashlib(root, info.nonce) == info.value >= thr
         assert info.n_devices == G and 0 <= info.winner_device < G
@@ -61,6 +66,7 @@ def main(n_search, which):
                                   "mean_over_nonces_done": round(sum(late_l) / max(1, sum(done)), 5)},
            "late_nonces_winner": {"p50": pct(late_w, 50), "p99": pct(late_w, 99)},
            "finish_ms_p50": round(pct(ttw, 50) / 1e3, 3),
+           "result_ms_p50": round(pct(res_ms, 50), 3),
            "distinct_winners": len(set(winners)), "kills_relayed": kills,
            "mean_nonces_done": round(statistics.mean(done))}
     print(json.dumps(res), flush=True)

@@ -32,8 +32,13 @@ pytestmark = pytest.mark.gpu
 # First-found cancellation bounds on CU partitions (host-observed, npow_wait_info.stop_after_decide_us):
 # the kill's way to the waves (one poll, within an iteration of ~15 us), one or two more hashes, and the
 # losing worker's observation of its launch's end.  Measured on the MI355X: see DESIGN.md section 5.
-P50_BOUND_US = 300.0
-P99_BOUND_US = 1500.0
+# The span is host-observed: with 8 logical devices, 8 pool workers poll one HIP runtime for their launches'
+# ends, and it grows with the device count (p50 ~0.1 ms over 4 partitions, ~0.35 ms over 8).
+BOUNDS_US = {4: (300.0, 1500.0), 8: (700.0, 1500.0)}  # devices -> (p50, p99)
+
+
+def bounds(g):
+    return BOUNDS_US[4] if g <= 4 else BOUNDS_US[8]
 
 
 def _child(script, env_extra, *args, timeout=110):
@@ -90,11 +95,12 @@ def test_first_win_overshoot_bound_cu_partitions(g):
     assert out["ok"] and out["devices"] == g and out["kills_relayed"] > 0
     assert all(first >= 0 for _hip, first, _cus in out["partitions"]), out["partitions"]
     s = out["stop_after_decide_us"]
-    assert s["p50"] < P50_BOUND_US and s["p99"] < P99_BOUND_US, out
-    # the losers' waves hashed something after they knew (at least one hash of a workgroup), and no more
-    # than a few hashes of every workgroup of every losing device (2 x 512 lanes x 4 workgroups per CU)
+    p50, p99 = bounds(g)
+    assert s["p50"] < p50 and s["p99"] < p99, out
+    # counted in the kernels: the losers' workgroups hashed at most one hash each after they knew (the dead
+    # word's value is read after the hash its load hides behind): at most 512 lanes x 4 workgroups per CU
     late = out["late_nonces_losers"]
-    assert 0 < late["p50"] <= 2 * 512 * 4 * 256, out
+    assert 0 < late["p50"] <= 512 * 4 * 256, out
 
 
 def test_first_win_overshoot_time_shared_8_devices():
@@ -130,7 +136,8 @@ def test_physical_gpus_overshoot_bound():
     out = _child("overshoot_worker.py", {"NANOPOW_VIRTUAL_DEVICES": None}, "200", "receive")
     assert out["ok"] and out["devices"] == n and out["kills_relayed"] > 0
     s = out["stop_after_decide_us"]
-    assert s["p50"] < P50_BOUND_US and s["p99"] < P99_BOUND_US, out
+    p50, p99 = bounds(n)
+    assert s["p50"] < p50 and s["p99"] < p99, out
 
 
 def test_physical_gpus_burst_64():

@@ -317,3 +317,29 @@ def test_cpu_workers_beside_the_gpu():
     out = json.loads(p.stdout.strip().splitlines()[-1])
     print(json.dumps(out))
     assert out["ok"] and out["mixed_receive"]["cpu_nonces"] > 0
+
+
+def test_wait_result_returns_at_the_decision(gpu_engine):
+    """npow_wait_result (ABI 4): the outcome as soon as it is known -- a re-validated winner, a cancellation,
+    an exhausted range -- with the ticket still valid for npow_wait, which then returns the same outcome and
+    the complete nonce count."""
+    eng = gpu_engine
+    M64 = (1 << 64) - 1
+    rng = random.Random(41)
+    for _ in range(8):
+        root = bytes(rng.getrandbits(8) for _ in range(32))
+        t = eng.submit(root, 0xfffffe0000000000, start=rng.getrandbits(64), device_mask=1)
+        r = t.wait_result(30)
+        assert r.status == _lib.NPOW_OK and oracle.work_value_hashlib(root, r.nonce) == r.value >= 0xfffffe0000000000
+        f = t.wait(30)
+        assert f.status == _lib.NPOW_OK and (f.nonce, f.value) == (r.nonce, r.value) and f.nonces_done > 0
+    tok = _lib.CancelToken()
+    t = eng.submit(bytes(range(32)), M64, device_mask=1, cancel=tok)
+    assert t.wait_result(0.2) is None
+    tok.set()
+    assert t.wait_result(10).status == _lib.NPOW_CANCELLED
+    assert t.wait(10).status == _lib.NPOW_CANCELLED
+    t = eng.submit(bytes(32), M64, start=5, device_mask=1, max_nonces_per_device=100_000)
+    assert t.wait_result(30).status == _lib.NPOW_EXHAUSTED
+    f = t.wait(30)
+    assert f.status == _lib.NPOW_EXHAUSTED and f.nonces_done == 100_000
