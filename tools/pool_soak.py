@@ -44,8 +44,10 @@ def main():
     ap.add_argument("--clients", type=int, default=24)
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--faults", action="store_true", help="a fault hook is set: bounded ranges over every device")
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU workers beside the GPU(s) (npow_config_cpu_threads): every mask-0 search also runs on them")
     args = ap.parse_args()
-    eng = _lib.Engine()
+    eng = _lib.Engine(cpu_threads=args.cpu_threads)
     stop = time.time() + args.seconds
     counts = {"search": 0, "cancel_token": 0, "cancel_ticket": 0, "abandoned": 0, "bounded": 0, "sweep": 0,
               "reconfig": 0}
@@ -68,9 +70,13 @@ def main():
             try:
                 if kind < 0.45:
                     thr = rng.choice([0xfffff00000000000, 0xfffffe0000000000, 0xffffff0000000000, 0xfffffff800000000])
-                    r = eng.submit(root, thr, start=rng.getrandbits(64)).wait(120)
+                    t = eng.submit(root, thr, start=rng.getrandbits(64))
+                    early = t.wait_result(120) if rng.random() < 0.5 else None  # the outcome at the decision
+                    r = t.wait(120)
                     if r is None or r.status != _lib.NPOW_OK or eng.work_value(root, r.nonce) != r.value or r.value < thr:
                         fail(f"search {root.hex()} {thr:016x}: {r}")
+                    if early is not None and (early.status, early.nonce, early.value) != (r.status, r.nonce, r.value):
+                        fail(f"wait_result {early} differs from wait {r}")
                     bump("search")
                 elif kind < 0.65:
                     tok = _lib.CancelToken()
