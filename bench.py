@@ -146,8 +146,8 @@ def issue_bound_cycles(mix):
     full = mix["valu"] - adds - aligns
     return 4 * (adds + aligns + max(0, full - aligns) / 2)
 # rocprofv3 PMC passes of the bench's own command (tools/pmc_bench.sh), newest first
-PMC_POOL = ("r04f_pmc_pool.json", "r03s_pmc_pool.json", "r03w_pmc_pool.json", "r03p_pmc_pool.json", "r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
-PMC_SWEEP = ("r04f_pmc_sweep.json", "r03s_pmc_sweep.json", "r03w_pmc_sweep.json", "r03p_pmc_sweep.json", "r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
+PMC_POOL = ("r04f_pmc_pool.json", "r04e_pmc_pool.json", "r03s_pmc_pool.json", "r03w_pmc_pool.json", "r03p_pmc_pool.json", "r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
+PMC_SWEEP = ("r04f_pmc_sweep.json", "r04e_pmc_sweep.json", "r03s_pmc_sweep.json", "r03w_pmc_sweep.json", "r03p_pmc_sweep.json", "r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
 METRIC = "Gnonce/s blake2b-64 per GPU & 8-GPU node; p50 time-to-work at fffffff8"
 CSRC = os.path.join(HERE, "nano-dpow_amd", "csrc")
 
@@ -181,12 +181,16 @@ def timed_region_profile(build: str):
         avg = re.search(r"timed region = the last (\d+) dispatches.*?average ([0-9.]+) ms", txt)
         npl = re.search(r"^nonces_per_launch ([0-9]+)", txt, re.M)
         fr = re.search(r"^frac_executed_from_profile ([0-9.]+)", txt, re.M)
+        cy = re.search(r"^cycles_per_hash_from_profile ([0-9.]+)", txt, re.M)
+        mz = re.search(r"^in_kernel_mhz ([0-9.]+)", txt, re.M)
         if not (m and avg and npl):
             continue
         parsed.append({"file": "profiles/" + os.path.basename(f), "build_sha16": m.group(1),
                        "matches_this_build": m.group(1) == build, "timed_dispatches": int(avg.group(1)),
                        "avg_dispatch_ms": float(avg.group(2)), "nonces_per_launch": int(npl.group(1)),
-                       "frac_from_profile": float(fr.group(1)) if fr else None})
+                       "frac_from_profile": float(fr.group(1)) if fr else None,
+                       "in_kernel_mhz": float(mz.group(1)) if mz else None,
+                       "cycles_per_hash_from_profile": float(cy.group(1)) if cy else None})
     for p in parsed:
         if p["matches_this_build"]:
             return p
@@ -705,7 +709,9 @@ def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, ke
                          "SQ_ACTIVE_INST_VALU2), which the stream's priority runs exploit; the GPU's power cap "
                          "holds its clock below 2.4 GHz meanwhile (sclk_mhz): issue_model holds the bound that "
                          "applies to this instruction mix",
-            "profile": (dict(prof, recompute=f"frac = nonces_per_launch x {ex} / avg_dispatch_ms / {PEAK_TOPS:.3f} Tops/s")
+            "profile": (dict(prof, recompute=f"frac = nonces_per_launch x {ex} / avg_dispatch_ms / {PEAK_TOPS:.3f} Tops/s; "
+                                             "the fraction follows the box's power-limited clock, so compare "
+                                             "cycles_per_hash_from_profile with issue_model.kernel_cycles_per_hash")
                         if prof else None),
             "traffic": (pmc or {}).get("hbm_bytes_per_launch"),
             "traffic_unit": "HBM bytes per launch, rocprofv3 FETCH_SIZE/WRITE_SIZE passes "
@@ -1504,6 +1510,8 @@ def main() -> int:
     if args.workload == "search" and WORLD == 1 and args.gpus == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline()
     recv_cpu = receive_cpu_legs(args) if args.workload == "receive" else None
+    if cpu or recv_cpu:
+        time.sleep(1.0)  # let the CPU legs' worker processes finish exiting before the GPU work is timed
 
     rank = int(os.environ.get("RANK", "0"))
     dist = None

@@ -665,11 +665,13 @@ void Worker::check_slots() {
           j.cancel_req = true;
           decide_locked(j, NPOW_CANCELLED);
         }
+        // No launch holds the job on this device (adopted, waiting for the next launch's table): it hashes
+        // nothing more of it, from now.  Otherwise the stop time (Job::t_stop) is taken when this worker sees
+        // it stop hashing: its final count published, or the last launch that held it completed (retire()).
+        // A launch queued behind another and started after the kill still hashes the job until one of its
+        // waves polls the kill word (within an iteration), so "not started at the decision" is no proof of zero.
+        if (sl.inflight.empty() && j.t_stop[sl.k] == 0) j.t_stop[sl.k] = now_us();
       }
-      // The job's stop time (Job::t_stop) is taken when this worker sees it stop hashing: its final
-      // count published, or the launches that held it retired (device_done_locked).  A launch queued
-      // behind another and started after the kill still hashes the job until one of its waves polls
-      // the kill word (within an iteration), so "not started at the decision" is no proof of zero.
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);  // in-flight waves stop
       sl.state = SlotState::kDraining;
       sl.stop_us = now_us();

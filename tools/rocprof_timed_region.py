@@ -50,6 +50,14 @@ def main():
           f"/ {peak} Tops/s = {npl * ex / (avg * 1e-3) / 1e12:.3f} Tops/s / {peak}")
     if "frac_algorithmic" in ro:
         print(f"frac_algorithmic_from_profile {npl * 2232 / (avg * 1e-3) / 1e12 / peak:.4f} (2,232 ops per nonce)")
+    # the box-independent figure: the fraction follows the box's power-limited clock (2,150-2,370 MHz by box),
+    # the SIMD cycles per 64-nonce wave-hash do not (1,024 SIMDs x 64 lanes)
+    mhz = b.get("sclk_mhz", {}).get("mean")
+    if mhz:
+        rate = npl / (avg * 1e-3)
+        print(f"in_kernel_mhz {mhz}")
+        print(f"cycles_per_hash_from_profile {1024 * 64 * mhz * 1e6 / rate:.1f}"
+              f"  = 1,024 SIMDs x 64 lanes x {mhz} MHz / ({npl} nonces / {avg:.4f} ms)")
 
 
 if __name__ == "__main__":
