@@ -129,7 +129,9 @@ struct PoolTable {
   uint32_t counted;       // search kernels: workgroups are counted on their entries (early finish,
                           // dynamic entries).  The host sets it for tables of 2 or more entries: a
                           // launch with one entry ends with it, and counting only slows its end.
-  uint32_t pad[6];
+  uint32_t kill_base;     // the low half of PoolMailbox::kills when the table was built: a polling wave that
+                          // reads another value relays the kill words of every entry, not only its own
+  uint32_t pad[5];
   PoolEntry e[kMaxSlots];
 };
 inline size_t pool_table_bytes(uint32_t n) { return offsetof(PoolTable, e) + (size_t)n * sizeof(PoolEntry); }
@@ -216,6 +218,9 @@ struct PoolMailbox {
   // dynamic entries published (ring positions, see PoolDynEntry).  One word, so a poll reads both
   // with one uncached read.
   alignas(64) uint64_t ctl;
+  // Bumped by the host after it raises any kill word of this device (round 4): a poll lands on one entry,
+  // and with n live entries a kill of another entry would wait ~n polls for a wave on that entry.
+  alignas(64) uint64_t kills;
   alignas(64) PoolClk clk[4][kClkWaves];  // [launch ring][XCD] (host: kEventRing == 4)
 };
 

@@ -538,9 +538,18 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
                                          uint32_t* seen) {
   const ConstEntry* pe = ls2_entry(tab, mb, e);
   const uint64_t ctl = ls2_ctl(mb);
+  const uint32_t kills = (uint32_t)__hip_atomic_load(&mb->kills, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const uint32_t nd = ls2_dyn_count(tab, ctl);
   ls2_fresh(nd, seen);
   bool leave = false;
+  if (kills != tab->kill_base) {  // a job of this launch was killed since it was built: relay every such entry
+    for (uint32_t k = 0; k < tab->n + nd; ++k) {
+      ConstEntry* q = ls2_entry(tab, mb, k);
+      if (__hip_atomic_load(&mb->kill[q->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q->gen &&
+          load_dead(st, q->slot) < q->gen)
+        ls2_kill(st, mb, q->slot, q->gen, tab->counted != 0);
+    }
+  }
   if ((ctl >> 32) != (tab->yield_base >> 32)) {
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
       ConstEntry* q = ls2_entry(tab, mb, k);

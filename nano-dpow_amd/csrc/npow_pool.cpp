@@ -249,6 +249,7 @@ void stop_other_devices_locked(Job& j, size_t k_win) {
                                                                       // read the decision themselves)
     Device& d = *g_devs[(size_t)j.devs[k]];
     __atomic_store_n(&d.pmb->kill[j.dev_slot[k]], j.dev_gen[k], __ATOMIC_RELEASE);
+    __atomic_fetch_add(&d.pmb->kills, 1ull, __ATOMIC_RELEASE);  // after the kill word: every poll then relays it
     std::lock_guard<std::mutex> sg(d.stats_mu);
     d.kills_relayed++;
   }
@@ -657,6 +658,7 @@ void Worker::check_slots() {
         push_back_locked(sl, 0, true);
       }
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);
+      __atomic_fetch_add(&d_.pmb->kills, 1ull, __ATOMIC_RELEASE);
       sl.state = SlotState::kDraining;
     } else if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {
       {
@@ -673,6 +675,7 @@ void Worker::check_slots() {
         if (sl.inflight.empty() && j.t_stop[sl.k] == 0) j.t_stop[sl.k] = now_us();
       }
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);  // in-flight waves stop
+      __atomic_fetch_add(&d_.pmb->kills, 1ull, __ATOMIC_RELEASE);
       sl.state = SlotState::kDraining;
       sl.stop_us = now_us();
     } else if (sl.no_more) {
@@ -721,6 +724,7 @@ int Worker::launch() {
   // final count would reach the host ~60 us after the launch's own end; measured with
   // NANOPOW_TRACE_LATENCY).  Two or more: a won entry's job need not wait for the others.
   t.counted = n >= 2 ? 1u : 0u;
+  t.kill_base = (uint32_t)__atomic_load_n(&d_.pmb->kills, __ATOMIC_ACQUIRE);
   ++seq_;
   t.ring = (uint32_t)ring_;
   t.seq = (uint32_t)seq_;
