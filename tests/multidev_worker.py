@@ -108,6 +108,14 @@ def main():
     sroot = bytes(range(9, 41))
     hits = eng.sweep(sroot, 0xffff000000000000, 1 << 40, (1 << 22) + 13, device_mask=0)
     assert hits == oracle.sweep(sroot, 0xffff000000000000, 1 << 40, (1 << 22) + 13)
+    # 6b. values through the shipped stream and per-lane pairs on the last device (a CU partition under
+    #     NANOPOW_VIRTUAL_DEVICES: its grid is sized to its CUs, its copies stay on its own stream)
+    vroot = bytes(range(70, 102))
+    vals = eng.values(vroot, (1 << 40) - 1000, 4099, device=G - 1)
+    assert vals == oracle.work_values([vroot] * 4099, [(1 << 40) - 1000 + i for i in range(4099)])
+    pr = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(257)]
+    pn = [rng.getrandbits(64) for _ in range(257)]
+    assert eng.values_pairs(pr, pn, device=G - 1) == oracle.work_values(pr, pn)
     # 7. a subset mask: devices 1 and 3 only
     for d in range(G):
         eng.reset_stats(d)
