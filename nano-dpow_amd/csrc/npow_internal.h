@@ -170,6 +170,10 @@ struct PoolDevState {
   PoolSlotCount count[kMaxSlots][kWgsShards];
   unsigned long long done[kMaxSlots][kPoolDoneShards * 8];  // nonces hashed (word 0) and late ones (word
                                                             // kLateWord), sharded over 64-B lines
+  // The low half of PoolMailbox::kills up to which some wave has relayed every kill word into the dead words
+  // (ls2_poll): one scan of the entries per kill, not one per poll (a 64-entry scan is 64 uncached reads).
+  alignas(64) unsigned long long kills_done;
+  uint8_t pad_kd[56];
 };
 
 // Pinned host-coherent mailbox of the pool: one win record per slot (the winner stores

@@ -545,13 +545,19 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
   const uint32_t nd = ls2_dyn_count(tab, ctl);
   ls2_fresh(nd, seen);
   bool leave = false;
-  if (kills != tab->kill_base) {  // a job of this launch was killed since it was built: relay every such entry
+  // A job of this launch was killed since it was built, and no wave has relayed that kill yet: relay every such
+  // entry (its dead word first, a device read; the kill word, uncached, only for live entries), then record the
+  // counter value so that the other polls skip the scan (round 4: scanning at every poll after a kill cost a
+  // 512-request burst 10 % of its kernel rate -- 64 serial uncached reads stalled each polling workgroup).
+  if (kills != tab->kill_base &&
+      (uint32_t)__hip_atomic_load(&st->kills_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kills) {
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
       ConstEntry* q = ls2_entry(tab, mb, k);
-      if (__hip_atomic_load(&mb->kill[q->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q->gen &&
-          load_dead(st, q->slot) < q->gen)
+      if (load_dead(st, q->slot) < q->gen &&
+          __hip_atomic_load(&mb->kill[q->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q->gen)
         ls2_kill(st, mb, q->slot, q->gen, tab->counted != 0);
     }
+    __hip_atomic_store(&st->kills_done, (unsigned long long)kills, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if ((ctl >> 32) != (tab->yield_base >> 32)) {
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
