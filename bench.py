@@ -1236,7 +1236,8 @@ def run_timed_inprocess(eng, n_dev: int, steps: int, warmup: int, thr: int = SEN
                 errors.append(f"search {idx} returned status {info.status}")
                 return
             with lock:
-                recs.append((dt, info.nonces_done, info.stop_after_decide_us, info.overshoot_nonces))
+                recs.append((dt, info.nonces_done, info.stop_after_decide_us, info.overshoot_nonces,
+                             info.late_nonces_losers))
     t0 = time.perf_counter()
     ths = [threading.Thread(target=client) for _ in range(n_dev)]
     for t in ths:
@@ -1251,13 +1252,20 @@ def run_timed_inprocess(eng, n_dev: int, steps: int, warmup: int, thr: int = SEN
             sum(k.nonces for k in ks), sum(k.launches for k in ks), ks)
 
 
-def overshoot_summary(spans_us, over_nonces, done):
-    return {"stop_after_decide_us": {"p50": round(pct(spans_us, 50), 1), "p99": round(pct(spans_us, 99), 1)},
-            "overshoot_nonces": {"p50": int(pct(over_nonces, 50)), "p99": int(pct(over_nonces, 99)),
-                                 "share_of_nonces": round(sum(over_nonces) / max(1, sum(done)), 5)},
-            "what": "per search, how long the other GPUs kept hashing after the host accepted the winner "
-                    "(host-observed: their final count or launch end seen by their worker -- an upper bound) "
-                    "and the nonces that span is worth at each GPU's kernel rate (npow_wait_info)"}
+def overshoot_summary(spans_us, over_nonces, done, late=None):
+    out = {"stop_after_decide_us": {"p50": round(pct(spans_us, 50), 1), "p99": round(pct(spans_us, 99), 1)},
+           "overshoot_nonces": {"p50": int(pct(over_nonces, 50)), "p99": int(pct(over_nonces, 99)),
+                                "share_of_nonces": round(sum(over_nonces) / max(1, sum(done)), 5)},
+           "what": "per search, how long the other GPUs kept hashing after the host accepted the winner "
+                   "(host-observed: their final count or launch end seen by their worker -- an upper bound) "
+                   "and the nonces that span is worth at each GPU's kernel rate (npow_wait_info)"}
+    if late is not None:
+        # counted in the kernels: the losers' hashes for the job after one of their waves knew it was over.  With
+        # several jobs in a launch the workgroups that leave a dead entry go on hashing the others, so the
+        # host-observed span above is mostly useful work; this is the waste
+        out["late_nonces_losers"] = {"p50": int(pct(late, 50)), "p99": int(pct(late, 99)),
+                                     "share_of_nonces": round(sum(late) / max(1, sum(done)), 6)}
+    return out
 
 
 def inprocess_node_ttw(eng, n_dev: int, m: int, thr: int = SEND):
@@ -1448,7 +1456,8 @@ def main_inprocess(eng, args) -> int:
     clk = sclk.summary()
     if clk:
         line["sysfs_sclk_mhz"] = clk
-    line["timed_overshoot"] = overshoot_summary([r[2] for r in recs], [r[3] for r in recs], [r[1] for r in recs])
+    line["timed_overshoot"] = overshoot_summary([r[2] for r in recs], [r[3] for r in recs], [r[1] for r in recs],
+                                                [r[4] for r in recs])
     if os.environ.get("NANOPOW_VIRTUAL_DEVICES"):
         parts = [[k.hip_device, k.cu_first, k.cus] for k in ks]
         if all(p[1] >= 0 for p in parts):
