@@ -640,7 +640,7 @@ def pmc_nonces_per_dispatch(pmc, valu_per_iteration):
     return c["SQ_INSTS_VALU"] / valu_per_iteration * 64
 
 
-LOOP_VALU = 5  # the search loop's VALU instructions per iteration besides the stream
+LOOP_VALU = 5.5  # the search loop's VALU per iteration besides the stream: 5, and 2 v_readlane at every 4th
 
 
 def result_line(world, steps, warmup, tot_nonces, max_wall, all_ttw, kern_ms, kern_nonces, launches, parallelism=None):

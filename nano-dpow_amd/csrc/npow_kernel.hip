@@ -681,7 +681,6 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     while (it < c.it_end) {
       const uint32_t verdict = __hip_atomic_load(&s_stop[sw], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       const uint64_t dead = __hip_atomic_load(dead_p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint64_t now = budget ? __builtin_amdgcn_s_memrealtime() : 0;
       // The verdict holds every request filed after the previous hashes: each was drained before the
       // s_barrier closing its iteration, which every wave passed before this read.  So all waves see the same
       // set here and leave together, before this hash (round 4; rounds 2-3 acted on it after the hash: one
@@ -729,8 +728,13 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
             __hip_atomic_load(&s_flag[wv], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT));
         why = (p & 2u) ? 2u : (why ? why : (p ? 3u : 0u));
       }
-      if (readlane64(dead, 0) == gen) why = 1u;
-      const bool late = budget && !c.bounded && (uint32_t)now - (uint32_t)t_start >= budget;
+      // the dead word in one v_cmp (readlane64 took two v_readlane and their SALU hazards), and the time budget
+      // at every fourth iteration: the launch's start clock lives in lanes of a VGPR (an SGPR spill) whose two
+      // v_readlane per iteration, with their s_nop hazards, cost 15 SIMD cycles per hash (-0.36 %,
+      // tools/experiments/loop_ab.py, profiles/r04_ab_loop.jsonl); a launch now ends up to ~45 us past its budget
+      if (__ballot(dead == gen) != 0) why = 1u;
+      const bool late = budget && !c.bounded && (it0 & 3u) == 0 &&
+                        (uint32_t)__builtin_amdgcn_s_memrealtime() - (uint32_t)t_start >= budget;
       if (__builtin_expect(why != 0 || late, 0)) {
         if (lane == 0)
           __hip_atomic_fetch_min(&s_stop[sw], (it << 2) | (late ? 0u : why), __ATOMIC_RELAXED,

@@ -259,6 +259,28 @@ def test_new_jobs_join_a_running_launch_and_finish_early(gpu_engine):
         gpu_engine.set_pool_tuning(budget_us=20_000)
 
 
+def test_launches_end_on_their_time_budget(gpu_engine):
+    """A pool launch ends when its time budget is spent (every wave compares s_memrealtime with the
+    launch's start, npow_kernel.hip pool_body_ls2), not at its iteration cap: a job that cannot win runs
+    in launches of the budget's length (HIP-event kernel times, npow_device_stats), to within a few
+    iterations of ~15 us."""
+    budget_ms = 4.0
+    gpu_engine.set_pool_tuning(budget_us=int(budget_ms * 1e3))
+    try:
+        tok = _lib.CancelToken()
+        t = gpu_engine.submit(bytes(range(32)), M64, device_mask=1, cancel=tok)
+        time.sleep(0.05)
+        gpu_engine.reset_stats(0)
+        time.sleep(0.3)
+        st = gpu_engine.stats(0)
+        tok.set()
+        assert t.wait(10).status == _lib.NPOW_CANCELLED
+        per = st.kernel_ms / max(1, st.launches)
+        assert st.launches >= 40 and budget_ms - 0.1 <= per <= budget_ms + 0.25, (st.launches, st.kernel_ms)
+    finally:
+        gpu_engine.set_pool_tuning(budget_us=20_000)
+
+
 def test_abandoned_ticket_is_cancelled_and_collected(gpu_engine):
     """A ticket dropped without wait() (a caller that gave up): its finaliser cancels the search
     and collects it, so the job leaves the pool and its cancel word is no longer read."""
