@@ -10,6 +10,6 @@ timeout -k 10 200 $PYT tests/test_gpu_multidevice.py::test_four_logical_devices 
 timeout -k 10 500 $PYT tests/test_gpu_configs.py > gpurun_out/${T}_pytest_gpu_configs_3_4.log 2>&1 &&
 ./tools/soaks_r04.sh $T &&
 ./tools/workloads_refresh.sh $T &&
-./tools/experiments/hwq_overshoot.sh
+if [ "${HWQ:-0}" = 1 ]; then ./tools/experiments/hwq_overshoot.sh; fi
 rc=$?
 tail -n 3 gpurun_out/${T}_pytest_gpu_configs_3_4.log; exit $rc
