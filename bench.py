@@ -56,6 +56,10 @@ Other BASELINE.json configurations (``--workload``; not the driver's default lin
   receive   config 1: single work_generate requests at receive difficulty fffffe0000000000,
             on the GPU (C ABI and HTTP server) next to the reference's CPU path
             (hashlib.blake2b, one core, and the oracle's C port on the host cores);
+  regime    the 8-GPU time regime: one root at a time at ffffffc0 (2^26 nonces, ~1.9 ms on
+            one GPU) over --gpus devices of the process, the next root submitted at the previous result;
+            time-to-work against ln2 * 2^26 / kernel rate, node rate against kernel rate, the per-search
+            fixed cost decomposed (node_ttw_8x_regime);
   dpow      the MQTT path end to end: --roots work messages at
             fffffff8 arriving as a Poisson stream at --rate per second, 25 % cancelled by
             a cancel message, delivered to the WorkHandler-equivalent (nanopow.dpow,
@@ -1154,11 +1158,12 @@ def fixed_overhead(eng, mask: int, rate: float, n: int = 300):
             "how": "receive-difficulty searches (fffffe00...) one at a time: wall time - nonces_done / kernel rate"}
 
 
-def latency_sample(eng, dev: int, n: int, rate_gnps=None):
+def latency_sample(eng, dev: int, n: int, rate_gnps=None, snap=None):
     """BASELINE config 2's time-to-work on a real sample: n first-win searches on R_0..R_{n-1} at
     fffffff8 through the C ABI, one at a time, after the timed region (not part of value), with the
     decomposition of its p50 / mean: the sample's own nonce counts against the exponential law's
-    (E = 2^29, median ln2 * 2^29), the fixed per-search overhead, and the kernel rate."""
+    (E = 2^29, median ln2 * 2^29), the fixed per-search overhead, and the kernel rate.  snap (optional):
+    called right after the n searches, before the overhead sample; its result is returned as out["_snap"]."""
     ttw, nn, coll = [], [], []
     t0 = time.perf_counter()
     for i in range(n):
@@ -1167,6 +1172,7 @@ def latency_sample(eng, dev: int, n: int, rate_gnps=None):
         coll.append(t_all)
         nn.append(info.nonces_done)
     wall = time.perf_counter() - t0
+    snapped = snap() if snap else None
     E = float(1 << 29)
     ln2 = 0.6931471805599453
     mean_n = statistics.mean(nn)
@@ -1197,7 +1203,33 @@ def latency_sample(eng, dev: int, n: int, rate_gnps=None):
                        "that p50_from_sample_nonces closes is the sample's luck, the rest is per-search cost"},
            "note": "npow_search at fffffff800000000 through the C ABI, one at a time, after the timed region; "
                    "not part of value"}
+    if snapped is not None:
+        out["_snap"] = snapped
     return out
+
+
+def steady_state(lat, leg, sampler, n):
+    """the rate at the card's power-capped steady state, beside the headline.  The driver's timed
+    region is ~0.2 s (20 searches) -- the card has not reached its power cap yet -- while the time-to-work leg runs
+    ~11 s of the same searches: value_steady = its nonces / its wall time (value's definition), with the kernel-counted
+    rate, the in-kernel clock of the same launches, the card's power, and the roofline fraction at 2.4 GHz and at
+    that clock (executed int32 ops, as roofline.frac)."""
+    ex = stream_mix()["executed_int32_ops"]
+    kg = leg.nonces / (leg.kernel_ms * 1e-3) / 1e9 if leg.kernel_ms > 0 else None
+    mhz = leg.clock_mhz or None
+    achieved = kg * ex / 1e3 if kg else None  # Tops/s
+    pw = sampler.power_summary()
+    return {"value": lat["gnps"], "unit": "Gnonce/s",
+            "kernel_gnps": round(kg, 4) if kg else None,
+            "in_kernel_mhz": round(mhz, 1) if mhz else None,
+            "frac": round(achieved / PEAK_TOPS, 4) if achieved else None,
+            "frac_at_measured_sclk": round(achieved / (256 * 128 * mhz * 1e6 / 1e12), 4) if achieved and mhz else None,
+            "power_w": pw,
+            "cycles_per_hash": round(1024 * 64 * mhz * 1e6 / (kg * 1e9), 1) if kg and mhz else None,
+            "what": f"the {n} time-to-work searches at fffffff8 after the timed region (ttw_c_abi_ms; ~11 s, the card "
+                    "at its power-capped steady state): value = their nonces / their wall time (the headline's "
+                    "definition), kernel_gnps = the kernels' count / their HIP-event time, frac = kernel rate x "
+                    f"{ex} executed int32 ops / 78.64 Tops/s (2.4 GHz) and at the in-kernel clock of those launches"}
 
 
 def run_timed_inprocess(eng, n_dev: int, steps: int, warmup: int, thr: int = SEND):
@@ -1252,6 +1284,19 @@ def run_timed_inprocess(eng, n_dev: int, steps: int, warmup: int, thr: int = SEN
             sum(k.nonces for k in ks), sum(k.launches for k in ks), ks)
 
 
+def device_check(rates, kernel_nonces, search_nonces):
+    """a multi-GPU run fails loudly rather than reporting a node rate with a slow or miscounting
+    device in it -- every device's kernel rate within 0.9x of the median, and the devices' nonce counters
+    (npow_device_stats) summing exactly to the nonces the searches report (nonces_done)."""
+    med = statistics.median(rates) if rates else 0.0
+    slow = [i for i, r in enumerate(rates) if r < 0.9 * med]
+    return {"ok": not slow and kernel_nonces == search_nonces,
+            "kernel_gnps": [round(r, 4) for r in rates], "median_gnps": round(med, 4), "slow_devices": slow,
+            "kernel_nonces": int(kernel_nonces), "search_nonces": int(search_nonces),
+            "what": "each device's kernel rate >= 0.9 x the median, and the device counters' nonces == the searches' "
+                    "nonces_done; bench.py exits non-zero otherwise"}
+
+
 def overshoot_summary(spans_us, over_nonces, done, late=None):
     out = {"stop_after_decide_us": {"p50": round(pct(spans_us, 50), 1), "p99": round(pct(spans_us, 99), 1)},
            "overshoot_nonces": {"p50": int(pct(over_nonces, 50)), "p99": int(pct(over_nonces, 99)),
@@ -1296,6 +1341,162 @@ def inprocess_node_ttw(eng, n_dev: int, m: int, thr: int = SEND):
             "note": f"one root at a time searched by all {n_dev} GPUs of the process on disjoint strides "
                     "(npow_submit over device_mask), first win cancelling the others; after the timed region, "
                     "not part of value"}
+
+
+REGIME = 0xffffffc000000000  # 2^-26 per nonce: fffffff8's 2^29 nonces split over 8 GPUs, on one GPU's rate
+
+
+def _mean_p(xs):
+    xs = [x for x in xs if x is not None]
+    if not xs:
+        return None
+    return {"mean": round(statistics.mean(xs), 1), "p50": round(pct(xs, 50), 1), "p99": round(pct(xs, 99), 1)}
+
+
+def node_regime(eng, n_dev: int, m: int, thr: int = REGIME, http_m: int = 0):
+    """the 8-GPU time regime on the devices of this process.  One root at a time over all n_dev
+    devices (disjoint strides, first win cancels the others), as the DPoW client's serial loop sends them
+    (client/work_handler.py:98-125): the next root is submitted as soon as the previous result is in (npow_wait_result,
+    what a client is answered with), and a reaper thread collects each ticket behind it (npow_wait_info: nonces and
+    timeline), as the JSON server does.  At ffffffc0 a search expects 2^26 nonces: ~1.9 ms on one MI355X, the time
+    scale of fffffff8 (2^29) on 8 GPUs -- so per-search fixed costs weigh what they would there.
+
+    Reports the C-ABI time-to-work against ln2 * 2^26 / the node's kernel rate, the node's rate against its kernel
+    rate, and the per-search fixed cost decomposed: the GPU idle between searches (HIP events), the host timeline of
+    each search (adopt, launch issue on the first / last device, the winner's record read, the decision, the result
+    in the client), the client's turnaround to the next submit, the losers' stop; optionally http_m requests over
+    one keep-alive connection (the HTTP hop)."""
+    import queue
+    mask = (1 << n_dev) - 1
+    for w in range(5):
+        search_to_result(eng, bench_root(6_900_000 + w), thr, bench_start(w), mask)
+    for d in range(n_dev):
+        eng.reset_stats(d)
+    q: "queue.Queue" = queue.Queue()
+    infos, errors = [], []
+
+    def reaper():
+        while True:
+            item = q.get()
+            if item is None:
+                return
+            try:
+                infos.append(item.wait_info())
+            except Exception as e:  # reported below
+                errors.append(repr(e))
+    th = threading.Thread(target=reaper, daemon=True)
+    th.start()
+    res, turn = [], []
+    t0 = time.perf_counter()
+    t_prev = None
+    for i in range(m):
+        idx = 6_000_000 + i
+        root = bench_root(idx)
+        t = time.perf_counter()
+        if t_prev is not None:
+            turn.append((t - t_prev) * 1e6)  # the client's turnaround: result in hand -> the next submit
+        tk = eng.submit(root, thr, start=bench_start(idx), device_mask=mask)
+        r = tk.wait_result()
+        t_prev = time.perf_counter()
+        if r is None or r.status != 0 or eng.work_value(root, r.nonce) != r.value or r.value < thr:
+            raise RuntimeError(f"regime search {idx}: bad result {r}")
+        res.append(t_prev - t)
+        q.put(tk)
+    q.put(None)
+    th.join()
+    wall = time.perf_counter() - t0
+    if errors:
+        raise RuntimeError("; ".join(errors[:4]))
+    ks = [eng.stats(d) for d in range(n_dev)]
+    done = [x.nonces_done for x in infos]
+    kern_rate = sum(k.nonces / (k.kernel_ms * 1e-3) for k in ks if k.kernel_ms > 0)  # node: devices side by side
+    node_gnps = sum(done) / wall / 1e9
+    ln2 = 0.6931471805599453
+    E = float(1 << 64) / float((1 << 64) - thr)
+    per_search_us = wall / m * 1e6
+    hashing_us = statistics.mean(done) / kern_rate * 1e6
+    idle = [k.idle_ms * 1e3 / k.idle_gaps for k in ks if k.idle_gaps]
+    line = {
+        "threshold": f"{thr:016x}", "devices": n_dev, "searches": m,
+        "c_abi_ttw_ms": {"p50": round(pct(res, 50) * 1e3, 4), "p99": round(pct(res, 99) * 1e3, 4),
+                         "mean": round(statistics.mean(res) * 1e3, 4)},
+        "kernel_gnps": round(kern_rate / 1e9, 4),
+        "node_gnps": round(node_gnps, 4),
+        "node_over_kernel": round(node_gnps * 1e9 / kern_rate, 4),
+        "expected_p50_ms": round(ln2 * E / kern_rate * 1e3, 4),
+        "expected_mean_ms": round(E / kern_rate * 1e3, 4),
+        "p50_minus_expected_ms": round(pct(res, 50) * 1e3 - ln2 * E / kern_rate * 1e3, 4),
+        "nonces_per_search_over_E": round(statistics.mean(done) / E, 4),
+        "fixed_cost_us": {
+            "per_search_wall_us": round(per_search_us, 1),
+            "hashing_at_kernel_rate_us": round(hashing_us, 1),
+            "fixed_us": round(per_search_us - hashing_us, 1),
+            "what": "wall time per search minus its nonces at the node's kernel rate: what the parts below make up"},
+        "decomposition_us": {
+            "gpu_idle_between_launches": {
+                "mean_per_gap": round(statistics.mean(idle), 1) if idle else None,
+                "per_device": [round(x, 1) for x in idle],
+                "what": "each device's stream from one launch's stop event to the next one's start event (HIP "
+                        "events; libnanopow npow_device_stats idle_ms / idle_gaps): with one search per launch, "
+                        "the device's idle time per search"},
+            "adopt": _mean_p([x.adopt_us for x in infos]),
+            "launch_first_device": _mean_p([x.launch_us for x in infos]),
+            "launch_last_device": _mean_p([x.launch_all_us or None for x in infos]),
+            "win_seen": _mean_p([x.win_seen_us for x in infos]),
+            "win_seen_to_decided": _mean_p([x.decide_us - x.win_seen_us for x in infos if x.win_seen_us > 0]),
+            "decided_to_result_in_client": _mean_p([r * 1e6 - x.decide_us for r, x in zip(res, infos)]),
+            "client_turnaround_to_next_submit": _mean_p(turn),
+            "losers_stop_after_decide": _mean_p([x.stop_after_decide_us for x in infos]),
+            "collected_after_submit": _mean_p([x.finish_us for x in infos]),
+            "what": "host timeline of each search, us since its npow_submit (npow_wait_info, steady clock) -- adopt "
+                    "(a device's worker took the job), launch issued on the first / last device, the winning "
+                    "device's win record read by the host (the worker's poll: it naps up to 50 us between looks "
+                    "once a launch is 0.4 ms old), decided after CPU re-validation, the result in the client's "
+                    "thread (Python), the client's turnaround to the next submit, the losing devices' stop as the "
+                    "host saw it, the ticket collected (every device stopped)"},
+        "late_nonces_losers": _mean_p([x.late_nonces_losers for x in infos]),
+        "per_device_kernel_gnps": [round(k.nonces / (k.kernel_ms * 1e-3) / 1e9, 4) if k.kernel_ms > 0 else None
+                                   for k in ks],
+        "in_kernel_mhz": round(statistics.mean([k.clock_mhz for k in ks if k.clock_mhz > 0]), 1)
+        if any(k.clock_mhz > 0 for k in ks) else None,
+        "worker_core_share": round(sum(k.host_cpu_ms for k in ks) / max(1e-9, ks[0].host_wall_ms), 3),
+        "partitions": [[k.hip_device, k.cu_first, k.cus] for k in ks],
+    }
+    if http_m:
+        http = _http_ttw(eng, http_m, thr=thr, base=6_500_000, device_mask=mask)
+        line["http_keepalive_ttw_ms"] = {"p50": round(pct(http, 50) * 1e3, 4), "p99": round(pct(http, 99) * 1e3, 4),
+                                         "n": len(http),
+                                         "hop_p50_ms": round((pct(http, 50) - pct(res, 50)) * 1e3, 4)}
+    return line
+
+
+def workload_regime(eng, args, rank, world, dist):
+    """--workload regime: node_regime over --gpus devices of this process (default every visible one)."""
+    if world > 1:
+        raise SystemExit("--workload regime runs in ONE process (it drives every device itself)")
+    n_dev = args.gpus if args.gpus > 1 else eng.n_devices
+    thr = int(args.threshold, 16) if args.threshold else REGIME
+    reg = node_regime(eng, n_dev, args.steps, thr, http_m=args.http_requests)
+    rate = reg["node_gnps"]
+    ks = [eng.stats(d) for d in range(n_dev)]
+    line = result_line(n_dev, args.steps, 5, int(rate * 1e9), 1.0, [reg["c_abi_ttw_ms"]["p50"] / 1e3],
+                       sum(k.kernel_ms for k in ks), sum(k.nonces for k in ks), sum(k.launches for k in ks),
+                       parallelism=f"in-process x{n_dev}: one root at a time split over {n_dev} devices, first win "
+                                   "cancels the others (no collective)")
+    line.pop("max_ttw_ms", None)
+    line["unit"] = "Gnonce/s"
+    line["scaling"] = "strong"
+    line["p50_ttw_ms"], line["p99_ttw_ms"] = reg["c_abi_ttw_ms"]["p50"], reg["c_abi_ttw_ms"]["p99"]
+    line["mean_ttw_ms"], line["n_ttw"] = reg["c_abi_ttw_ms"]["mean"], args.steps
+    line["roofline"]["kernel_gnps"] = reg["kernel_gnps"]
+    line["config"]["workload"] = (f"8-GPU time regime (VERDICT r04 #1): one root at a time at {reg['threshold']} over "
+                                  f"{n_dev} devices, the next root submitted at the previous result")
+    line["config"]["threshold"] = reg["threshold"]
+    line["node_ttw_8x_regime"] = reg
+    if os.environ.get("NANOPOW_VIRTUAL_DEVICES"):
+        line["virtual_devices_note"] = (f"NANOPOW_VIRTUAL_DEVICES: the {n_dev} devices are CU partitions of one GPU "
+                                        "(CU-masked streams), each launch on CUs of its own as on separate GPUs")
+    return line
 
 
 def workload_receive(eng, args, rank, world, dist):
@@ -1473,9 +1674,14 @@ def main_inprocess(eng, args) -> int:
                 "those of separate GPUs (a rehearsal of the path)")
     line["early_finishes"] = sum(k.early_finishes for k in ks)
     line["kills_relayed"] = sum(k.kills_relayed for k in ks)
+    line["device_check"] = device_check([k.nonces / (k.kernel_ms * 1e-3) / 1e9 if k.kernel_ms > 0 else 0.0 for k in ks],
+                                        kern_nonces, nonces)
     if args.node_searches:
         line["node_ttw_ms"] = inprocess_node_ttw(eng, n, args.node_searches)
     print(json.dumps(line), flush=True)
+    if not line["device_check"]["ok"]:
+        print(f"bench.py: device check failed: {line['device_check']}", file=sys.stderr)
+        return 3
     return 0
 
 
@@ -1490,7 +1696,8 @@ def main() -> int:
     ap.add_argument("--iters", type=int, default=0, help="override the search launch iteration cap")
     ap.add_argument("--budget-us", type=int, default=-1, help="override the search launch budget (0 = off)")
     ap.add_argument("--workload", default="search",
-                    choices=["search", "allgpus", "sweep", "burst", "sustained", "dpow", "receive"])
+                    choices=["search", "allgpus", "sweep", "burst", "sustained", "dpow", "receive", "regime"])
+    ap.add_argument("--threshold", default="", help="regime: threshold in hex (default ffffffc000000000)")
     ap.add_argument("--sweep-bits", type=int, default=36, help="sweep: range [0, 2^bits)")
     ap.add_argument("--roots", type=int, default=4096, help="burst: requests per GPU")
     ap.add_argument("--duration", type=float, default=60.0, help="sustained: seconds")
@@ -1544,7 +1751,8 @@ def main() -> int:
     dev = 0  # a rank's only visible GPU; in one process, devices 0..N-1
     if args.workload != "search":
         fn = {"allgpus": workload_allgpus, "sweep": workload_sweep, "burst": workload_burst,
-              "sustained": workload_sustained, "dpow": workload_dpow, "receive": workload_receive}[args.workload]
+              "sustained": workload_sustained, "dpow": workload_dpow, "receive": workload_receive,
+              "regime": workload_regime}[args.workload]
         line = fn(eng, args, rank, WORLD, dist)
         if recv_cpu:
             line["receive"].update(recv_cpu)
@@ -1573,25 +1781,28 @@ def main() -> int:
     with SclkSampler(dev) as sclk:
         res = run_timed(search, stats, lambda: eng.reset_stats(dev), args.steps, args.warmup, rank, WORLD, dist)
     st = timed_stats[-1]
-    local = (st.clock_mhz, st.host_cpu_ms / st.host_wall_ms if st.host_wall_ms > 0 else 0.0)
+    local = (st.clock_mhz, st.host_cpu_ms / st.host_wall_ms if st.host_wall_ms > 0 else 0.0,
+             st.nonces / (st.kernel_ms * 1e-3) / 1e9 if st.kernel_ms > 0 else 0.0)
     if dist is not None:
         gathered = [None] * WORLD
         dist.all_gather_object(gathered, local)
     else:
         gathered = [local]
     kern_rate = res[4] / (res[3] * 1e-3) / 1e9 if res[3] > 0 else None
-    lat, lat_clk = None, None
+    lat, lat_clk, steady = None, None, None
     if WORLD == 1 and args.latency_searches:
         # the card's clock and power over the ~11-s time-to-work leg too (the timed region is ~0.2 s at the
         # driver's 20 steps: a handful of samples), every 25 ms, with the in-kernel clock of the same launches
         eng.reset_stats(dev)
         with SclkSampler(dev, period=0.025, span="over the time-to-work leg") as lat_sclk:
-            lat = latency_sample(eng, dev, args.latency_searches, kern_rate)
+            lat = latency_sample(eng, dev, args.latency_searches, kern_rate, snap=lambda: eng.stats(dev))
+        leg = lat.pop("_snap")
         lat_clk = {"sysfs_sclk_mhz": lat_sclk.summary(), "sysfs_power_w": lat_sclk.power_summary(),
                    "in_kernel_mhz": round(eng.stats(dev).clock_mhz, 1),
                    "what": f"the {args.latency_searches} time-to-work searches (ttw_c_abi_ms; ~11 s of launches at "
                            "fffffff8 and the receive-difficulty overhead sample) sampled every 25 ms; the in-kernel "
                            "clock of their launches beside"}
+        steady = steady_state(lat, leg, lat_sclk, args.latency_searches)
     http = _http_ttw(eng, args.http_requests) if (rank == 0 and WORLD == 1 and args.http_requests) else None
     node = None
     if dist is not None and args.node_searches > 0 and int(os.environ.get("LOCAL_WORLD_SIZE", WORLD)) == WORLD:
@@ -1612,6 +1823,9 @@ def main() -> int:
             line["ttw_c_abi_ms"] = lat
         if lat_clk:
             line["ttw_leg_clock_power"] = lat_clk
+        if steady:
+            line["value_steady"] = steady["value"]
+            line["steady_state"] = steady
         if node:
             line["node_ttw_ms"] = node
         if http:
@@ -1621,11 +1835,16 @@ def main() -> int:
                                    "session), after the timed region; not part of value"}
         if cpu:
             line["cpu_baseline"] = cpu
+        line["device_check"] = device_check([g[2] for g in gathered], res[4], res[0])
         print(json.dumps(line), flush=True)
+    rc = 0
+    if rank == 0 and not line["device_check"]["ok"]:
+        print(f"bench.py: device check failed: {line['device_check']}", file=sys.stderr)
+        rc = 3
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 if __name__ == "__main__":

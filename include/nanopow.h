@@ -57,8 +57,12 @@ extern "C" {
  * 4: npow_config_cpu_threads (CPU workers, --cpu-threads), npow_wait_result (the outcome at the decision);
  * npow_device_stats gains late_nonces,
  * hip_device, cu_first; npow_search_info gains late_nonces_losers / late_nonces_winner (both structs
- * are written up to the size the caller passes, so revision-3 callers are unaffected). */
-#define NPOW_ABI_VERSION 4
+ * are written up to the size the caller passes, so revision-3 callers are unaffected).
+ * 5: npow_search_info gains the search's host timeline (adopt_us, launch_us, launch_all_us, win_seen_us);
+ * npow_device_stats gains idle_ms / idle_gaps (the GPU idle between the device's search launches) and
+ * affinity_checks / affinity_failures (NANOPOW_TEST_HOOKS=1: the calling thread's HIP device checked at every HIP
+ * call site of the device).  Both structs are still written up to the size the caller passes. */
+#define NPOW_ABI_VERSION 5
 
 /* Hash paths of npow_values_path. */
 #define NPOW_PATH_SEARCH 0  /* the instruction stream the search and sweep kernels execute
@@ -103,6 +107,13 @@ typedef struct npow_device_stats {
   int32_t hip_device;       /* HIP device this logical device runs on (-1: the CPU workers) */
   int32_t cu_first;         /* -1: the whole GPU; else the first CU of its partition (NANOPOW_VIRTUAL_DEVICES:
                                a CU-masked stream over CUs [cu_first, cu_first + cus)) */
+  /* ---- ABI 5 ---- */
+  double idle_ms;           /* GPU idle on the device's stream between consecutive search launches: from one
+                               launch's stop event to the next one's start event (HIP events), summed */
+  uint64_t idle_gaps;       /* ... over this many pairs of consecutive launches */
+  uint64_t affinity_checks; /* NANOPOW_TEST_HOOKS=1: HIP call sites of this device at which the calling thread's
+                               current HIP device was checked (hipGetDevice == hip_device) ... */
+  uint64_t affinity_failures; /* ... and found wrong (the call then fails: NPOW_ERR_INTERNAL) */
 } npow_device_stats;
 
 /* Outcome of one search (npow_wait_info).  Times are host steady-clock microseconds since
@@ -128,6 +139,12 @@ typedef struct npow_search_info {
                                    over (the kill relayed into their dead word); the host-side bound above
                                    adds the kill's way there and the worker's observation */
   uint64_t late_nonces_winner;  /* the same on the deciding device after its own win */
+  /* ---- ABI 5: the search's host timeline (us since npow_submit; 0 = it did not happen) ---- */
+  double adopt_us;          /* the first device's pool worker took the job */
+  double launch_us;         /* the first launch holding it was issued (any device) */
+  double launch_all_us;     /* every device of the job had issued a launch holding it */
+  double win_seen_us;       /* the deciding device's winner record was read by the host (decide_us follows its CPU
+                               re-validation) */
 } npow_search_info;
 
 /* CPU workers (nano-work-server.exe @1681064 `--cpu-threads N`): before npow_init, ask it to add

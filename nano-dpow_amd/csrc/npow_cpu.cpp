@@ -35,6 +35,14 @@ namespace {
 constexpr uint64_t kCpuClaim = 1ull << 16;  // nonces per claim (~20 ms of one thread)
 constexpr uint64_t kCpuCheck = 256;         // nonces between two looks at the stop conditions (~80 us)
 constexpr auto kCpuSupervise = std::chrono::microseconds(100);
+// Test hook (with NANOPOW_TEST_HOOKS=1): NANOPOW_TEST_CPU_RELEASE_DELAY_US=n holds the coordinator for n us between
+// its hashing threads' return and its look at the job (tests/fault_worker.py cpu_last: a GPU that dies in that window
+// hands its ranges to this device, which must hash them before the job can end)
+const long g_release_delay_us = [] {
+  const char* e = test_hooks_enabled() ? getenv("NANOPOW_TEST_CPU_RELEASE_DELAY_US") : nullptr;
+  if (e) fprintf(stderr, "nanopow: TEST HOOKS ACTIVE: CPU workers release their job %s us late\n", e);
+  return e ? atol(e) : 0L;
+}();
 
 struct CpuShared {
   std::mutex m;
@@ -57,8 +65,9 @@ bool over(const Job& j, const CpuShared& sh) {
          g_exiting.load(std::memory_order_relaxed);
 }
 
-// One hashing thread's share of the current job.
-void hash_job(CpuShared& sh, const JobP& jp, size_t k) {
+// One hashing thread's share of the current job.  Each claim's nonces go into the device's statistics as soon as
+// they are hashed (at the job's end only, a long unbounded search showed 0 nonces for the CPU device).
+void hash_job(CpuShared& sh, Device& d, const JobP& jp, size_t k) {
   Job& j = *jp;
   for (;;) {
     Range r{0, 0};
@@ -98,11 +107,15 @@ void hash_job(CpuShared& sh, const JobP& jp, size_t k) {
       if (stopped) break;
     }
     sh.hashed.fetch_add(n, std::memory_order_relaxed);
+    {
+      std::lock_guard<std::mutex> sg(d.stats_mu);
+      d.nonces += n;
+    }
     if (stopped) return;  // the rest of this claim is not hashed: the job is over for this device
   }
 }
 
-void hasher(CpuShared& sh) {
+void hasher(CpuShared& sh, Device& d) {
   uint64_t seen = 0;
   for (;;) {
     JobP j;
@@ -115,7 +128,7 @@ void hasher(CpuShared& sh) {
       j = sh.job;
       k = sh.k;
     }
-    hash_job(sh, j, k);
+    hash_job(sh, d, j, k);
     std::lock_guard<std::mutex> lk(sh.m);
     if (--sh.active == 0) sh.done_cv.notify_all();
   }
@@ -137,7 +150,11 @@ void cpu_worker_run(Device& d) {
   CpuShared sh;
   std::vector<std::thread> threads;
   threads.reserve((size_t)d.cpu_threads);
-  for (int i = 0; i < d.cpu_threads; ++i) threads.emplace_back([&sh] { hasher(sh); });
+  for (int i = 0; i < d.cpu_threads; ++i) threads.emplace_back([&sh, &d] { hasher(sh, d); });
+  {
+    std::lock_guard<std::mutex> g(d.cpu_tids_mu);  // their CPU time goes into the device's host_cpu_ms
+    for (auto& t : threads) d.cpu_tids.push_back(t.native_handle());
+  }
   for (;;) {
     JobP j;
     size_t k = 0;
@@ -161,6 +178,8 @@ void cpu_worker_run(Device& d) {
       j->on_dev[k] = 1;
       j->seen_dev[k] = 1;
       j->dev_slot[k] = -1;  // no kill word: the hashers read the job's decision themselves
+      if (j->t_launch == 0) j->t_launch = now_us();
+      if (j->t_launch_dev[k] == 0) j->t_launch_dev[k] = now_us();
     }
     d.worker_busy.store(true, std::memory_order_release);
     d.active_slots.store(1, std::memory_order_release);
@@ -171,22 +190,31 @@ void cpu_worker_run(Device& d) {
       std::lock_guard<std::mutex> g(sh.hit_mu);
       sh.hit = false;
     }
-    {
-      std::lock_guard<std::mutex> lk(sh.m);
-      sh.job = j;
-      sh.k = k;
-      sh.active = d.cpu_threads;
-      ++sh.epoch;
-    }
-    sh.cv.notify_all();
-    for (;;) {
+    // Hash the job in epochs: the hashing threads return once this device's queue of ranges is empty (or the job
+    // is over), and only then does this thread take g_pool.mu.  A GPU that died in between may have handed its
+    // unfinished ranges to this device (abandon_locked: the CPU is the last survivor) -- releasing the job then
+    // would end it EXHAUSTED with those ranges never hashed, so a new epoch hashes them first.
+    for (bool again = true; again;) {
       {
-        std::unique_lock<std::mutex> lk(sh.m);
-        if (sh.done_cv.wait_for(lk, kCpuSupervise, [&] { return sh.active == 0; })) break;
+        std::lock_guard<std::mutex> lk(sh.m);
+        sh.job = j;
+        sh.k = k;
+        sh.active = d.cpu_threads;
+        ++sh.epoch;
       }
-      if (over(*j, sh) || !g_pool.running) sh.stop = true;
+      sh.cv.notify_all();
+      for (;;) {
+        {
+          std::unique_lock<std::mutex> lk(sh.m);
+          if (sh.done_cv.wait_for(lk, kCpuSupervise, [&] { return sh.active == 0; })) break;
+        }
+        if (over(*j, sh) || !g_pool.running) sh.stop = true;
+        std::lock_guard<std::mutex> g(g_pool.mu);
+        release_unadopted_locked(d.id);
+      }
+      if (g_release_delay_us > 0) std::this_thread::sleep_for(std::chrono::microseconds(g_release_delay_us));
       std::lock_guard<std::mutex> g(g_pool.mu);
-      release_unadopted_locked(d.id);
+      again = !over(*j, sh) && g_pool.running && !j->todo[k].empty();
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     const uint64_t hashed = sh.hashed.load();
@@ -200,8 +228,7 @@ void cpu_worker_run(Device& d) {
     }
     {
       std::lock_guard<std::mutex> sg(d.stats_mu);
-      d.launches++;  // jobs hashed
-      d.nonces += hashed;
+      d.launches++;  // jobs hashed (their nonces went into d.nonces claim by claim)
       d.kernel_ms += ms;
     }
     d.active_slots.store(0, std::memory_order_release);
@@ -218,6 +245,10 @@ void cpu_worker_run(Device& d) {
       decide_locked(*j, NPOW_CANCELLED);
     }
     device_done_locked(j, k);
+  }
+  {
+    std::lock_guard<std::mutex> g(d.cpu_tids_mu);  // no CPU clock of a joined thread is read after this
+    d.cpu_tids.clear();
   }
   {
     std::lock_guard<std::mutex> lk(sh.m);

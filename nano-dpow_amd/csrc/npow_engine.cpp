@@ -83,7 +83,49 @@ std::vector<Device*> select_gpus(uint64_t mask) {
   return out;
 }
 
+thread_local bool t_pool_worker = false;  // this thread is a device's pool worker (Worker::run)
+
+int check_device_slow(Device& d, const char* site) {
+  // NANOPOW_TEST_AFFINITY_SKEW=d (with the test hooks): device d's pool worker expects the HIP device after its own,
+  // so that the check's failure path runs on a one-GPU box, where every logical device is HIP device 0
+  static const int skew = [] {
+    const char* e = getenv("NANOPOW_TEST_AFFINITY_SKEW");
+    if (e) fprintf(stderr, "nanopow: TEST HOOKS ACTIVE: device %s's pool worker expects the wrong HIP device\n", e);
+    return e ? atoi(e) : -1;
+  }();
+  int cur = -1;
+  const hipError_t e = hipGetDevice(&cur);
+  d.affinity_checks.fetch_add(1, std::memory_order_relaxed);
+  const int want = d.hip_id + (d.id == skew && t_pool_worker ? 1 : 0);
+  if (e == hipSuccess && cur == want) return NPOW_OK;
+  d.affinity_failures.fetch_add(1, std::memory_order_relaxed);
+  fprintf(stderr, "nanopow: TEST HOOK: device affinity violated at %s: logical device %d runs on HIP device %d, "
+                  "the calling thread's current device is %d\n", site, d.id, want, cur);
+  return fail(NPOW_ERR_INTERNAL, std::string("HIP call for device ") + std::to_string(d.id) + " at " + site +
+                                     " from a thread whose current HIP device is " + std::to_string(cur));
+}
+
+int check_device_memory(const void* p, const Device& d, const char* what) {
+  hipPointerAttribute_t a{};
+  HIPTRY(hipPointerGetAttributes(&a, p));
+  if (a.type != hipMemoryTypeDevice || a.device != d.hip_id)
+    return fail(NPOW_ERR_HIP, std::string("device ") + std::to_string(d.id) + ": " + what + " is not device memory of HIP device " +
+                                  std::to_string(d.hip_id) + " (type " + std::to_string((int)a.type) + ", device " +
+                                  std::to_string(a.device) + ")");
+  return NPOW_OK;
+}
+
+int check_pinned_mapping(const void* host, const void* dev, const char* what) {
+  hipPointerAttribute_t a{};
+  HIPTRY(hipPointerGetAttributes(&a, host));
+  if (a.type != hipMemoryTypeHost || a.devicePointer != dev)
+    return fail(NPOW_ERR_HIP, std::string(what) + ": pinned host memory whose device mapping is not the pointer the "
+                                                 "kernels are given");
+  return NPOW_OK;
+}
+
 void account_launch(Device& d, int ring) {
+  (void)check_device(d, "account_launch");
   float ms = 0.f;
   if (hipEventElapsedTime(&ms, d.ev_start[ring], d.ev_stop[ring]) != hipSuccess) ms = 0.f;
   std::lock_guard<std::mutex> g(d.stats_mu);
@@ -109,6 +151,7 @@ struct Inflight {
 
 // Launch one chunk on d's stream bracketed by timing events.
 int launch_chunk(Device& d, Mode mode, const LaunchArgs& a, int ring, uint64_t* out) {
+  DEVCHECK(d, "launch_chunk");
   HIPTRY(hipEventRecord(d.ev_start[ring], d.stream));
   // the shipped stream's kernels: four 512-lane workgroups per CU; the seq values kernel: 256-lane ones
   HIPTRY(launch_task(mode, mode == Mode::kValuesSeq ? grid_of(d) : ls_grid(d), d.stream, a, d.st, d.mb_dev, out));
@@ -118,6 +161,7 @@ int launch_chunk(Device& d, Mode mode, const LaunchArgs& a, int ring, uint64_t* 
 
 // Wait for every in-flight launch, accounting its time.
 int drain(Device& d, std::deque<Inflight>& q) {
+  DEVCHECK(d, "drain");
   HIPTRY(hipStreamSynchronize(d.stream));
   while (!q.empty()) {
     account_launch(d, q.front().ring);
@@ -127,6 +171,7 @@ int drain(Device& d, std::deque<Inflight>& q) {
 }
 
 int read_state(Device& d, DevState* hs) {
+  DEVCHECK(d, "read_state");
   HIPTRY(hipMemcpyAsync(hs, d.st, sizeof(DevState), hipMemcpyDeviceToHost, d.stream));
   HIPTRY(hipStreamSynchronize(d.stream));
   std::lock_guard<std::mutex> g(d.stats_mu);
@@ -135,6 +180,7 @@ int read_state(Device& d, DevState* hs) {
 }
 
 int reset_task(Device& d) {
+  DEVCHECK(d, "reset_task");
   HIPTRY(hipMemsetAsync(d.st, 0, sizeof(DevState), d.stream));
   HIPTRY(hipStreamSynchronize(d.stream));
   store_release(&d.mb->found, 0);
@@ -231,15 +277,21 @@ int init_device(Device& d, int n_physical, int parts) {
   } else {
     HIPTRY(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
   }
+  DEVCHECK(d, "init_device");
   HIPTRY(hipMalloc(&d.st, sizeof(DevState)));
   HIPTRY(hipMalloc(&d.d_out, kValuesChunk * sizeof(uint64_t)));
+  if (int rc = check_device_memory(d.st, d, "the task state")) return rc;
+  if (int rc = check_device_memory(d.d_out, d, "the hit / values buffer")) return rc;
   void* mb = nullptr;
   HIPTRY(hipHostMalloc(&mb, sizeof(HostMailbox), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
   memset(mb, 0, sizeof(HostMailbox));
   d.mb = (HostMailbox*)mb;
+  // the device pointer taken with d.hip_id current (hipSetDevice above; DEVCHECK under the test hooks), and
+  // checked against the allocation's own mapping
   void* mbd = nullptr;
   HIPTRY(hipHostGetDevicePointer(&mbd, mb, 0));
   d.mb_dev = (HostMailbox*)mbd;
+  if (int rc = check_pinned_mapping(mb, mbd, "the task mailbox")) return rc;
   for (int r = 0; r < kEventRing; ++r) {
     HIPTRY(hipEventCreate(&d.ev_start[r]));
     HIPTRY(hipEventCreate(&d.ev_stop[r]));
@@ -254,6 +306,7 @@ int device_sweep(Device& d, const RootPrecomp& pre, uint64_t threshold, uint64_t
                  bool& cancelled) {
   TaskLock lk(d);
   HIPTRY(hipSetDevice(d.hip_id));
+  DEVCHECK(d, "device_sweep");
   int rc = reset_task(d);
   if (rc) return rc;
   LaunchArgs a{};
@@ -433,13 +486,21 @@ int npow_set_pool_tuning(uint32_t budget_us, uint32_t blocks_per_cu) try {
   return NPOW_OK;
 } catch (...) { return guard_exception(); }
 
-// CPU time (ms) the device's pool worker thread has used so far (0 if unavailable).
-static double worker_cpu_ms(Device& d) {
-  if (!d.worker.joinable()) return 0.0;
+static double thread_cpu_ms(pthread_t t) {
   clockid_t cid;
   timespec ts;
-  if (pthread_getcpuclockid(d.worker.native_handle(), &cid) != 0 || clock_gettime(cid, &ts) != 0) return 0.0;
+  if (pthread_getcpuclockid(t, &cid) != 0 || clock_gettime(cid, &ts) != 0) return 0.0;
   return ts.tv_sec * 1e3 + ts.tv_nsec * 1e-6;
+}
+
+// CPU time (ms) the device's pool worker thread has used so far (0 if unavailable); for the CPU device, its
+// hashing threads' too.
+static double worker_cpu_ms(Device& d) {
+  if (!d.worker.joinable()) return 0.0;
+  double ms = thread_cpu_ms(d.worker.native_handle());
+  std::lock_guard<std::mutex> g(d.cpu_tids_mu);
+  for (pthread_t t : d.cpu_tids) ms += thread_cpu_ms(t);
+  return ms;
 }
 
 // A job that finished early (npow_pool.cpp early_finish) returns before the launch that held it
@@ -479,6 +540,10 @@ static int stats_fill(int device, npow_device_stats* out) {
   out->late_nonces = d.late;
   out->hip_device = d.hip_id;
   out->cu_first = d.cu_first;
+  out->idle_ms = d.idle_ms;
+  out->idle_gaps = d.idle_gaps;
+  out->affinity_checks = d.affinity_checks.load(std::memory_order_relaxed);
+  out->affinity_failures = d.affinity_failures.load(std::memory_order_relaxed);
   return NPOW_OK;
 }
 
@@ -507,6 +572,8 @@ int npow_device_stats_reset(int device) try {
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
   d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = d.kills_relayed = d.late = 0;
+  d.idle_gaps = 0;
+  d.idle_ms = 0.0;
   d.kernel_ms = 0.0;
   d.clk_ticks = d.clk_ref_ticks = 0.0;
   d.stats_t0 = std::chrono::steady_clock::now();
@@ -674,6 +741,7 @@ static int values_on(int device, const uint8_t root[32], uint64_t start, uint64_
   Device& d = *g_devs[device];
   TaskLock lk(d);
   HIPTRY(hipSetDevice(d.hip_id));
+  DEVCHECK(d, "values");
   int rc = reset_task(d);
   if (rc) return rc;
   LaunchArgs a{};
@@ -728,6 +796,7 @@ int npow_values_pairs(int device, const uint8_t* roots, const uint64_t* nonces, 
   Device& d = *g_devs[device];
   TaskLock lk(d);
   HIPTRY(hipSetDevice(d.hip_id));
+  DEVCHECK(d, "values_pairs");
   // chunks of kPairsChunk pairs through device buffers allocated once per call; every copy on the
   // device's own stream (a CU-partitioned logical device's stream is a blocking one, so the null
   // stream would wait for the other partitions' launches)

@@ -2,6 +2,7 @@
 // values, C ABI) and the work pool (npow_pool.cpp: concurrent first-win searches).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <pthread.h>
 
 #include <atomic>
 #include <chrono>
@@ -63,6 +64,8 @@ struct Device {
   uint64_t yields = 0, dyn = 0;            // launches yielded / jobs that joined a running launch
   uint64_t kills_relayed = 0;              // losing jobs stopped by another device's decision (npow_pool.cpp)
   uint64_t late = 0;                       // device-side overshoot: nonces hashed after the job was known over
+  double idle_ms = 0.0;                    // GPU idle between consecutive search launches (HIP events) ...
+  uint64_t idle_gaps = 0;                  // ... over this many pairs (npow_pool.cpp Worker::retire)
   // Published by the pool worker for npow_device_stats_get: it has launches or slots in flight, and
   // how many of its slots are still searching.  A job finished early returns before the launch that
   // held it is retired; with no slot searching, the stats wait for the worker to retire the rest.
@@ -77,6 +80,12 @@ struct Device {
   std::atomic<bool> dead{false};
   int dead_code = NPOW_ERR_HIP;  // the error a job gets when no device is left to search it
   std::string dead_msg;
+  // Test hook (NANOPOW_TEST_HOOKS=1): HIP call sites of this device at which the calling thread's current HIP
+  // device was checked, and how many were wrong (check_device below)
+  std::atomic<uint64_t> affinity_checks{0}, affinity_failures{0};
+  // CPU device (cpu_threads > 0): its hashing threads, for their CPU time in the stats (npow_cpu.cpp)
+  std::mutex cpu_tids_mu;
+  std::vector<pthread_t> cpu_tids;
 };
 
 extern std::vector<std::unique_ptr<Device>> g_devs;
@@ -135,6 +144,26 @@ void account_launch(Device& d, int ring);
 
 // ---- work pool (npow_pool.cpp) ----------------------------------------------------------------
 bool test_hooks_enabled();          // NANOPOW_TEST_HOOKS=1: the NANOPOW_FAULT_* hooks are honoured
+
+// Device affinity.  Every logical device runs on HIP device hip_id, and its HIP calls must come
+// from a thread whose current device is that one: streams, events and memory belong to a device, and on one
+// physical GPU (every test box so far) a call from the wrong device would pass unnoticed.  With test hooks on, each
+// HIP call site of a device checks hipGetDevice() == d.hip_id (counted in npow_device_stats.affinity_checks); a
+// mismatch is reported on stderr and the call fails with NPOW_ERR_INTERNAL (affinity_failures).  Without the hooks
+// the check costs nothing.  DESIGN.md section 5 lists the call sites and the threads that reach them.
+int check_device_slow(Device& d, const char* site);
+extern thread_local bool t_pool_worker;  // set by a device's pool worker thread (npow_pool.cpp Worker::run)
+inline int check_device(Device& d, const char* site) {
+  return test_hooks_enabled() ? check_device_slow(d, site) : NPOW_OK;
+}
+#define DEVCHECK(d, site)                                          \
+  do {                                                             \
+    if (int rc_ = ::npow::check_device((d), (site))) return rc_;   \
+  } while (0)
+// At npow_init (always): device memory of d must be owned by HIP device d.hip_id, and the pinned mailboxes must map
+// to the device pointers the kernels are given (hipPointerGetAttributes).
+int check_device_memory(const void* p, const Device& d, const char* what);
+int check_pinned_mapping(const void* host, const void* dev, const char* what);
 int pool_device_init(Device& d);     // allocate pool buffers of one device
 void pool_device_free(Device& d);
 void pool_start();                   // start one worker thread per device

@@ -165,15 +165,29 @@ struct PoolSlotCount {
 // entry in iterations that started after one of its waves knew the entry was over (its dead word, a win, or a
 // kill read by its poll), added when it leaves the entry.  Cumulative per slot like the done counts.
 constexpr int kLateWord = 1;
+// Workgroups that have left an uncounted (one-entry) launch, per launch ring (round 5): one counter per XCD
+// shard (workgroup index mod kWgsShards), then one over the shards, each on its own line -- the last one out
+// of a shard bumps `top`, the last one out of the launch publishes the entry's final count when the entry is
+// over (PoolMailbox::fin, as the counted launches' last leaver does), so a won or killed one-entry job
+// finishes without waiting for its launch's event and the done-count read-back behind it.  Every counter is
+// back at 0 when its launch ends (the last one out resets it), ready for the ring's next launch.
+struct PoolExit {
+  unsigned long long shard[kWgsShards][8];
+  unsigned long long top;
+  uint8_t pad[56];
+};
+constexpr int kPoolRing = 4;  // launch ring of the pool kernels (host: kEventRing)
 struct PoolDevState {
   PoolSlotWord slot[kMaxSlots];
   PoolSlotCount count[kMaxSlots][kWgsShards];
   unsigned long long done[kMaxSlots][kPoolDoneShards * 8];  // nonces hashed (word 0) and late ones (word
                                                             // kLateWord), sharded over 64-B lines
-  // The low half of PoolMailbox::kills up to which some wave has relayed every kill word into the dead words
-  // (ls2_poll): one scan of the entries per kill, not one per poll (a 64-entry scan is 64 uncached reads).
-  alignas(64) unsigned long long kills_done;
-  uint8_t pad_kd[56];
+  // Per launch ring: (the launch's seq << 32) | the low half of PoolMailbox::kills up to which a wave of THAT
+  // launch has relayed every kill word of its entries into the dead words (ls2_poll): one scan per kill and
+  // launch, not one per poll (a 64-entry scan is 64 uncached reads).  Keyed by launch: a launch
+  // holding other entries must not skip the scan because another launch relayed up to the same count.
+  alignas(64) unsigned long long kills_done[kPoolRing][8];
+  PoolExit exits[kPoolRing];
 };
 
 // Pinned host-coherent mailbox of the pool: one win record per slot (the winner stores
@@ -225,7 +239,7 @@ struct PoolMailbox {
   // Bumped by the host after it raises any kill word of this device (round 4): a poll lands on one entry,
   // and with n live entries a kill of another entry would wait ~n polls for a wave on that entry.
   alignas(64) uint64_t kills;
-  alignas(64) PoolClk clk[4][kClkWaves];  // [launch ring][XCD] (host: kEventRing == 4)
+  alignas(64) PoolClk clk[kPoolRing][kClkWaves];  // [launch ring][XCD] (host: kEventRing == kPoolRing)
 };
 
 // Grid of a search launch: kLsGroups 512-lane workgroups per CU.  A "unit" is what an entry's share

@@ -440,9 +440,27 @@ __device__ __forceinline__ bool ls2_join(PoolDevState* st, PoolMailbox* mb, uint
   return false;
 }
 
-// The same leave by all 64 lanes of wave 0, with the workgroup's count: the checks and the sum of the
-// done shards load in parallel (one lane per shard) instead of ~40 round trips one after another --
-// the last leaver's publish is on the path of a won job's reply.
+// Wave 0, every lane: sum the slot's done shards and late words and publish the final count (PoolMailbox::fin).
+// Lanes 0..31 load the done shards, lanes 32..63 the late words of the same lines, in parallel (one lane per
+// shard) instead of ~40 round trips one after another -- the publish is on the path of a won job's reply.
+__device__ __forceinline__ void ls2_fin_wave(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
+                                             uint32_t lane) {
+  static_assert(kPoolDoneShards == 32, "one half-wave per counter");
+  unsigned long long t = __hip_atomic_load(&st->done[slot][(lane & 31) * 8 + (lane < 32 ? 0 : kLateWord)],
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int m = 16; m >= 1; m >>= 1) t += __shfl_xor(t, m);
+  const unsigned long long t_late = readlane64(t, 32);
+  if (lane == 0) {
+    __hip_atomic_store(&mb->fin[slot].total, (uint64_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mb->fin[slot].late, (uint64_t)t_late, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mb->fin[slot].gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// The same leave by all 64 lanes of wave 0, with the workgroup's count: the checks load in parallel, and the last
+// leaver of a dead entry publishes its final count (ls2_fin_wave).  An uncounted launch only adds the counts (its
+// end is counted by ls2_exit instead).
 __device__ __forceinline__ void ls2_leave_wave(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
                                                uint32_t sum, uint32_t late, bool counted) {
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -469,18 +487,48 @@ __device__ __forceinline__ void ls2_leave_wave(PoolDevState* st, PoolMailbox* mb
                     __hip_atomic_load(&st->count[slot][lane].wgs, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   ls2_complete();
   if (__ballot(busy) != 0) return;
-  // lanes 0..31: the done shards, lanes 32..63: the late words of the same lines; summed per half
-  static_assert(kPoolDoneShards == 32, "one half-wave per counter");
-  unsigned long long t = __hip_atomic_load(&st->done[slot][(lane & 31) * 8 + (lane < 32 ? 0 : kLateWord)],
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-  for (int m = 16; m >= 1; m >>= 1) t += __shfl_xor(t, m);
-  const unsigned long long t_late = readlane64(t, 32);
+  ls2_fin_wave(st, mb, slot, gen, lane);
+}
+
+// Wave 0 of every workgroup of an uncounted (one-entry) launch, at its end (round 5): leave the
+// launch's exit count (PoolExit: per XCD shard, then over the shards) after the workgroup's done add; the last
+// workgroup out publishes the entry's final count if the entry is over (a win, a kill relayed into its dead word)
+// -- every workgroup of the launch has added its count by then, and no later launch hashes a dead entry (its
+// workgroups check the dead word before their first hash), so the total is final.  The host then finishes the job
+// from that record (Worker::early_finish), instead of waiting for the launch's stop event and the read-back of the
+// done counts queued behind it (~0.2-0.35 ms over CU-masked streams).  An entry that is still
+// live (the time budget ended the launch) publishes nothing: the next launch goes on with it.  Two levels keep the
+// fan-in per word at 1 / 8 of the grid (one address takes ~18 ns per atomic: 1,024 exits on one word ~18 us).
+__device__ __noinline__ void ls2_exit(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t G, uint32_t g) {
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const uint32_t x = g % kWgsShards;
+  const uint32_t in_shard = G / kWgsShards + (x < G % kWgsShards ? 1u : 0u);
+  const uint32_t shards = G < (uint32_t)kWgsShards ? G : (uint32_t)kWgsShards;
+  PoolExit* ex = &st->exits[tab->ring & (kPoolRing - 1)];
+  uint32_t last = 0;
   if (lane == 0) {
-    __hip_atomic_store(&mb->fin[slot].total, (uint64_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&mb->fin[slot].late, (uint64_t)t_late, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&mb->fin[slot].gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    ls2_complete();  // the workgroup's done add first
+    unsigned long long* sc = &ex->shard[x][0];
+    const unsigned long long o = __hip_atomic_fetch_add(sc, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    ls2_complete();
+    if (o + 1 == in_shard) {
+      __hip_atomic_store(sc, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the ring's next launch
+      const unsigned long long t = __hip_atomic_fetch_add(&ex->top, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      ls2_complete();
+      if (t + 1 == shards) {
+        __hip_atomic_store(&ex->top, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = 1;
+      }
+    }
   }
+  if (!__builtin_amdgcn_readfirstlane(last)) return;
+  const PoolEntry* pe = &tab->e[0];  // the launch's only entry
+  const uint32_t slot = pe->slot;
+  const uint64_t gen = pe->gen;
+  const bool over = load_dead(st, slot) >= gen;
+  ls2_complete();
+  if (!__builtin_amdgcn_readfirstlane(over ? 1u : 0u)) return;
+  ls2_fin_wave(st, mb, slot, gen, lane);
 }
 
 __device__ __forceinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* mb, uint32_t slot, uint64_t gen,
@@ -549,15 +597,22 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
   // entry (its dead word first, a device read; the kill word, uncached, only for live entries), then record the
   // counter value so that the other polls skip the scan (round 4: scanning at every poll after a kill cost a
   // 512-request burst 10 % of its kernel rate -- 64 serial uncached reads stalled each polling workgroup).
-  if (kills != tab->kill_base &&
-      (uint32_t)__hip_atomic_load(&st->kills_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kills) {
+  // The scan's key is this launch's (seq, kills) (keyed by the count alone, a launch could skip the
+  // scan because another launch, holding other entries, had relayed up to the same count).  The kill words are
+  // read only after `kills` was compared (a control dependency: the loads are issued after its value returned,
+  // and they bypass the caches), so every kill the counter stands for is seen: the host raises a kill word
+  // before it bumps the counter (release).  The compiler barrier keeps them from being hoisted above it.
+  unsigned long long* const kd = &st->kills_done[tab->ring & (kPoolRing - 1)][0];
+  const unsigned long long key = ((unsigned long long)tab->seq << 32) | kills;
+  if (kills != tab->kill_base && __hip_atomic_load(kd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != key) {
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
       ConstEntry* q = ls2_entry(tab, mb, k);
       if (load_dead(st, q->slot) < q->gen &&
           __hip_atomic_load(&mb->kill[q->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q->gen)
         ls2_kill(st, mb, q->slot, q->gen, tab->counted != 0);
     }
-    __hip_atomic_store(&st->kills_done, (unsigned long long)kills, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(kd, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if ((ctl >> 32) != (tab->yield_base >> 32)) {
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
@@ -779,6 +834,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     ++seg;
   }
+  if (!counted && wv == 0) ls2_exit(tab, st, mb, G, g);  // the one-entry launch's end record (round 5)
   clk_end_ls2(tab, mb, t_start, wv);
 }
 

@@ -83,6 +83,9 @@ const double g_poll_us = [] {
 }();
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
 const bool g_trace_lat = getenv("NANOPOW_TRACE_LATENCY") != nullptr;
+// NANOPOW_TRACE_STEPS=1: each pool worker times the parts of its steps (adopt, check_slots, read-back, launch, retire,
+// nap) and prints count / total / max / calls over 50 us per part when it exits (diagnostics of the host path)
+const bool g_trace_steps = getenv("NANOPOW_TRACE_STEPS") != nullptr;
 // Fault injection (tests): see the header comment.
 struct Faults {
   uint64_t invalid_mask = 0;  // logical devices whose wins read back corrupted
@@ -327,6 +330,33 @@ class Worker {
   uint64_t yields_ = 0;
   uint64_t ctl_ = 0;  // PoolMailbox::ctl (only this worker writes it): yields << 32 | dynamic entries
   int invalid_streak_ = 0;  // consecutive winners of this device that failed CPU re-validation
+  int prev_stop_ring_ = -1;  // ring of the last retired launch (its stop event: the GPU idle before the next one),
+                             // -1 when a sweep / values task used the device's events since
+  struct StepProf {
+    uint64_t n = 0, slow = 0;
+    double total = 0, max = 0;
+  };
+  StepProf prof_[6];  // NANOPOW_TRACE_STEPS: adopt, check_slots, queue_readbacks, launch, retire, nap
+  template <class F>
+  auto timed(int part, F&& f) {
+    if (!g_trace_steps) return f();
+    const double t = now_us();
+    auto r = f();
+    const double dt = now_us() - t;
+    StepProf& p = prof_[part];
+    p.n++;
+    p.total += dt;
+    p.max = std::max(p.max, dt);
+    if (dt > 50.0) p.slow++;
+    return r;
+  }
+  void print_prof() const {
+    static const char* names[6] = {"adopt", "check_slots", "read-back", "launch", "retire", "nap"};
+    for (int i = 0; i < 6; ++i)
+      fprintf(stderr, "nanopow-steps[%d] %-11s n %llu total_ms %.1f mean_us %.2f max_us %.1f over50us %llu\n", d_.id,
+              names[i], (unsigned long long)prof_[i].n, prof_[i].total * 1e-3,
+              prof_[i].n ? prof_[i].total / prof_[i].n : 0.0, prof_[i].max, (unsigned long long)prof_[i].slow);
+  }
   std::unique_lock<std::mutex> dev_lock_{d_.mu, std::defer_lock};
 
   bool busy() const {
@@ -393,7 +423,7 @@ void Worker::adopt() {
     j->on_dev[k] = 1;
     j->dev_slot[k] = s;
     j->dev_gen[k] = sl.gen;
-    if (g_trace_lat && j->t_adopt == 0) j->t_adopt = now_us();
+    if (j->t_adopt == 0) j->t_adopt = now_us();
     sl.new_job = !j->seen_dev[k];
     if (sl.new_job) adopted = true;  // a new job: worth ending a long launch for
     j->seen_dev[k] = 1;
@@ -449,7 +479,11 @@ bool Worker::dyn_add(int s) {
   sl.inflight.push_back({f.seq, pe.base, pe.count});
   if (todo.empty()) sl.no_more = true;
   sl.fresh = false;
-  if (g_trace_lat && j.t_launch == 0) j.t_launch = now_us();
+  {
+    const double t = now_us();
+    if (j.t_launch == 0) j.t_launch = t;
+    if (j.t_launch_dev[sl.k] == 0) j.t_launch_dev[sl.k] = t;
+  }
   ctl_ = (ctl_ & ~0xffffffffull) | (uint32_t)(ctl_ + 1);  // the low half wraps on its own
   __atomic_store_n(&d_.pmb->ctl, ctl_, __ATOMIC_RELEASE);  // after the entry
   {
@@ -495,6 +529,7 @@ void Worker::yield_if_long() {
 
 // A win published for slot s (this generation): CPU re-validation decides the job.
 void Worker::handle_win(int s) {
+  const double t_seen = now_us();
   Slot& sl = slots_[s];
   Job& j = *sl.job;
   PoolWin& pw = d_.pmb->win[s];
@@ -504,12 +539,13 @@ void Worker::handle_win(int s) {
   if ((faults().invalid_mask >> d_.id) & 1) v ^= 1;  // NANOPOW_FAULT_INVALID (tests)
   const uint64_t cpu_v = host_work_value(j.pre.m, n);
   std::lock_guard<std::mutex> g(g_pool.mu);
-  if (g_trace_lat && j.t_win == 0) j.t_win = now_us();
+  if (j.t_win == 0) j.t_win = t_seen;
   if (cpu_v == v && v >= j.threshold) {
     invalid_streak_ = 0;
     if (j.status == kPending) {
       decide_locked(j, NPOW_OK, n, v);
       j.t_decide = now_us();
+      j.t_win_seen = t_seen;
       j.winner_k = (int)sl.k;
       stop_other_devices_locked(j, sl.k);
     }
@@ -571,6 +607,7 @@ uint64_t Worker::push_back_locked(Slot& sl, size_t from, bool skip_done) {
 // right before it on the stream has fired (the launches ahead of it are done).
 bool Worker::launch_started(uint64_t seq) const {
   if (seq <= retired_seq_) return true;
+  (void)check_device(d_, "launch_started");
   for (const PoolInflight& f : q_)
     if (f.seq == seq) return hipEventQuery(d_.ev_start[f.ring]) == hipSuccess;
   return false;
@@ -581,6 +618,7 @@ bool Worker::launch_started(uint64_t seq) const {
 // failed: never in q_) has not.
 bool Worker::launch_completed(uint64_t seq) const {
   if (seq <= retired_seq_) return true;
+  (void)check_device(d_, "launch_completed");
   for (const PoolInflight& f : q_)
     if (f.seq == seq) return hipEventQuery(d_.ev_stop[f.ring]) == hipSuccess;
   return false;
@@ -730,6 +768,7 @@ int Worker::launch() {
   t.seq = (uint32_t)seq_;
   {
     std::lock_guard<std::mutex> g(g_pool.mu);  // issued[] is shared with other workers' reads
+    const double t_issue = now_us();
     for (uint32_t e = 0; e < n; ++e) {
       Slot& sl = slots_[idx[e]];
       Job& j = *sl.job;
@@ -758,7 +797,8 @@ int Worker::launch() {
       r.count -= pe.count;
       if (r.count == 0) todo.pop_front();
       sl.inflight.push_back({seq_, pe.base, pe.count});
-      if (g_trace_lat && j.t_launch == 0) j.t_launch = now_us();
+      if (j.t_launch == 0) j.t_launch = t_issue;
+      if (j.t_launch_dev[sl.k] == 0) j.t_launch_dev[sl.k] = t_issue;
       if (todo.empty()) sl.no_more = true;
       sl.fresh = false;
     }
@@ -766,6 +806,7 @@ int Worker::launch() {
   const int r = ring_;
   ring_ = (ring_ + 1) % kEventRing;
   const size_t bytes = pool_table_bytes(n);
+  DEVCHECK(d_, "pool launch");
   // Up to kArgEntries entries the table rides in the kernel arguments (no copy before the launch;
   // uploading it instead cost 2.5 %, profiles/r02_ab_table_upload.jsonl); a larger one goes up in
   // stream order right before its launch.  (Uploading it on a second stream beside the running
@@ -794,6 +835,7 @@ int Worker::launch() {
 // launch that still holds them (later launches do not), and note when that copy lands.
 int Worker::queue_readbacks() {
   constexpr size_t row = kPoolDoneShards * 8;
+  DEVCHECK(d_, "pool read-back");
   for (int s = 0; s < kMaxSlots; ++s) {
     Slot& sl = slots_[s];
     if (sl.state != SlotState::kDraining || sl.readback) continue;
@@ -806,11 +848,24 @@ int Worker::queue_readbacks() {
 }
 
 int Worker::retire() {
+  DEVCHECK(d_, "pool retire");
   while (!q_.empty()) {
     const hipError_t e = hipEventQuery(d_.ev_stop[q_.front().ring]);
     if (e == hipErrorNotReady) break;
     if (e != hipSuccess) return fail(NPOW_ERR_HIP, std::string("pool launch: ") + hipGetErrorString(e));
     account_launch(d_, q_.front().ring);
+    // the GPU idle before this launch: the previous launch's stop event to this one's start event (the ring slot of
+    // the previous launch is not reused before this one retires: at most two launches are in flight)
+    if (prev_stop_ring_ >= 0) {
+      float gap = 0.f;
+      if (hipEventElapsedTime(&gap, d_.ev_stop[prev_stop_ring_], d_.ev_start[q_.front().ring]) == hipSuccess &&
+          gap >= 0.f) {
+        std::lock_guard<std::mutex> sg(d_.stats_mu);
+        d_.idle_ms += gap;
+        d_.idle_gaps++;
+      }
+    }
+    prev_stop_ring_ = q_.front().ring;
     account_clock(q_.front().ring, q_.front().seq);
     // The launch's ranges are complete, except those of a generation that won in it (or in an
     // earlier launch still unseen): handle such wins first, they hand back what did not finish.
@@ -921,26 +976,34 @@ void Worker::fail_all(const std::string& msg) {
     sl.state = SlotState::kFree;
   }
   q_.clear();
+  prev_stop_ring_ = -1;
 }
 
 int Worker::step() {
-  adopt();
-  check_slots();
-  if (int rc = queue_readbacks()) return rc;  // before the next launch: it no longer holds them
-  if (d_.tasks_waiting.load() == 0)            // a sweep / values call is waiting: drain instead
-    if (int rc = launch()) return rc;
-  if (int rc = retire()) return rc;
+  timed(0, [&] { adopt(); return 0; });
+  timed(1, [&] { check_slots(); return 0; });
+  if (int rc = timed(2, [&] { return queue_readbacks(); })) return rc;  // before the next launch: it no longer holds them
+  if (d_.tasks_waiting.load() == 0)                                       // a sweep / values call is waiting: drain instead
+    if (int rc = timed(3, [&] { return launch(); })) return rc;
+  if (int rc = timed(4, [&] { return retire(); })) return rc;
   publish_busy();
   return NPOW_OK;
 }
 
 void Worker::run() {
   prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);  // nap(): 1-us timer slack instead of the default 50 us
+  t_pool_worker = true;
   if (hipSetDevice(d_.hip_id) != hipSuccess) {
     d_.dead_code = NPOW_ERR_HIP;
     d_.dead_msg = "device " + std::to_string(d_.id) + ": hipSetDevice failed";
     d_.dead = true;
   }
+  struct OnExit {
+    const Worker& w;
+    ~OnExit() {
+      if (g_trace_steps) w.print_prof();
+    }
+  } on_exit{*this};
   for (;;) {
     if (g_exiting.load(std::memory_order_relaxed)) return;
     if (d_.dead && !busy()) {
@@ -976,6 +1039,7 @@ void Worker::run() {
     if (d_.tasks_waiting.load() > 0 && q_.empty()) {
       // hand the device to a waiting sweep / values call (TaskLock); lock() below then waits
       // for it to finish
+      prev_stop_ring_ = -1;  // the task records the device's events too
       if (dev_lock_.owns_lock()) dev_lock_.unlock();
       while (d_.tasks_waiting.load() > 0 && !g_exiting.load(std::memory_order_relaxed))
         std::this_thread::sleep_for(std::chrono::microseconds(50));
@@ -993,7 +1057,7 @@ void Worker::run() {
       if (dev_lock_.owns_lock()) dev_lock_.unlock();
       continue;
     }
-    nap();
+    timed(5, [&] { nap(); return 0; });
   }
 }
 
@@ -1045,17 +1109,23 @@ void Worker::nap() {
 
 // -- device resources -----------------------------------------------------------------------------
 int pool_device_init(Device& d) {
+  DEVCHECK(d, "pool_device_init");
   HIPTRY(hipMalloc(&d.pst, sizeof(PoolDevState)));
-  HIPTRY(hipMemset(d.pst, 0, sizeof(PoolDevState)));
+  if (int rc = check_device_memory(d.pst, d, "the pool state")) return rc;
+  // on the device's own stream, not the null stream: a CU-partitioned device's stream is a blocking one
+  HIPTRY(hipMemsetAsync(d.pst, 0, sizeof(PoolDevState), d.stream));
+  HIPTRY(hipStreamSynchronize(d.stream));
   void* mb = nullptr;
   HIPTRY(hipHostMalloc(&mb, sizeof(PoolMailbox), hipHostMallocCoherent | hipHostMallocMapped | hipHostMallocPortable));
   memset(mb, 0, sizeof(PoolMailbox));
   d.pmb = (PoolMailbox*)mb;
-  void* mbd = nullptr;
+  void* mbd = nullptr;  // taken with d.hip_id current (init_device), checked against the allocation's own mapping
   HIPTRY(hipHostGetDevicePointer(&mbd, mb, 0));
   d.pmb_dev = (PoolMailbox*)mbd;
+  if (int rc = check_pinned_mapping(mb, mbd, "the pool mailbox")) return rc;
   for (int r = 0; r < kEventRing; ++r) {
     HIPTRY(hipMalloc(&d.d_tab[r], sizeof(PoolTable)));
+    if (int rc = check_device_memory(d.d_tab[r], d, "a launch table")) return rc;
     void* h = nullptr;
     HIPTRY(hipHostMalloc(&h, sizeof(PoolTable), hipHostMallocDefault));
     memset(h, 0, sizeof(PoolTable));
@@ -1130,7 +1200,11 @@ void pool_stop() {
 // -- jobs -------------------------------------------------------------------------------------------
 int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
                 uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket) {
-  auto devs = select_devices(device_mask);
+  // A bounded search over "all devices" (mask 0) leaves the CPU workers out: their stride would be as
+  // long as a GPU's at ~1/1000 of its rate, nothing hands their leftover to an idle GPU, and they work on one job
+  // at a time -- an exhausting search would wait for them.  An explicit mask may still name the CPU device.
+  auto devs = max_nonces_per_device && device_mask == 0 ? select_gpus(0) : select_devices(device_mask);
+  if (devs.empty() && max_nonces_per_device && device_mask == 0) devs = select_devices(0);  // only the CPU is left
   if (devs.empty()) return fail(NPOW_ERR_NO_DEVICE, "no usable device in device_mask");
   auto j = std::make_shared<Job>();
   j->pre = host_precompute(root);
@@ -1154,6 +1228,7 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   j->dev_slot.assign(G, -1);
   j->dev_gen.assign(G, 0);
   j->t_stop.assign(G, 0.0);
+  j->t_launch_dev.assign(G, 0.0);
   j->late.assign(G, 0);
   j->pending_devs = (int)G;
   j->t_submit = now_us();
@@ -1216,6 +1291,19 @@ int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* va
       if ((int)k != j->winner_k) dev_late += j->late[k];
     info->late_nonces_losers = dev_late;
     info->late_nonces_winner = j->winner_k >= 0 ? j->late[(size_t)j->winner_k] : 0;
+    auto since = [&](double t) { return t > 0 ? t - j->t_submit : 0.0; };
+    info->adopt_us = since(j->t_adopt);
+    info->launch_us = since(j->t_launch);
+    double all = 0.0;
+    for (size_t k = 0; k < j->devs.size(); ++k) {
+      if (j->t_launch_dev[k] == 0) {  // a device that never launched it (decided before it got to it; the CPU device)
+        all = 0.0;
+        break;
+      }
+      all = std::max(all, j->t_launch_dev[k]);
+    }
+    info->launch_all_us = since(all);
+    info->win_seen_us = since(j->t_win_seen);
   }
   if (g_trace_lat) {
     fprintf(stderr, "nanopow-lat adopt %.1f launch %.1f win %.1f kend %.1f finish %.1f return %.1f", j->t_adopt - j->t_submit,

@@ -38,6 +38,7 @@ struct Job {
   std::vector<int> dev_slot;        // per device k: the slot holding it while on_dev[k] ...
   std::vector<uint64_t> dev_gen;    // ... and its generation there (the decider raises their kill words)
   std::vector<double> t_stop;       // per device k: when its worker saw it stop hashing the job (us; 0 = never adopted)
+  std::vector<double> t_launch_dev; // per device k: when its first launch holding the job was issued (us; 0 = none)
   std::vector<uint64_t> late;       // per device k: nonces its waves hashed after they knew the job was over
                                     // (device-side count, PoolDevState kLateWord)
   int winner_k = -1;                // the device whose result decided the job
@@ -56,9 +57,10 @@ struct Job {
   std::atomic<bool> cancel_req{false};
 
   bool cancel_seen() const { return cancel_req.load(std::memory_order_relaxed) || (cancel && load_acquire(cancel)); }
-  // host timestamps of the job's life (steady clock, us): t_submit, t_decide and t_finish always
-  // (npow_wait_info), the rest for NANOPOW_TRACE_LATENCY, which prints them in pool_wait
-  double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0, t_decide = 0;
+  // host timestamps of the job's life (steady clock, us): npow_wait_info reports them (t_kend only for
+  // NANOPOW_TRACE_LATENCY, which prints the timeline in pool_wait).  t_win: the first win record read; t_win_seen:
+  // the deciding one (CPU re-validation then decides at t_decide)
+  double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0, t_decide = 0, t_win_seen = 0;
 };
 using JobP = std::shared_ptr<Job>;
 

@@ -30,7 +30,7 @@ NPOW_ERR_INVALID_WORK = -5
 NPOW_ERR_CAPACITY = -6
 NPOW_ERR_INTERNAL = -7
 
-NPOW_ABI_VERSION = 4
+NPOW_ABI_VERSION = 5
 # hash paths of npow_values_path
 NPOW_PATH_SEARCH = 0   # the stream the search and sweep kernels execute (four 512-lane workgroups per CU)
 NPOW_PATH_SEQ = 1      # a second generated stream, scheduled without barriers
@@ -77,6 +77,10 @@ class DeviceStats(ctypes.Structure):
         ("late_nonces", ctypes.c_uint64),    # ABI 4
         ("hip_device", ctypes.c_int32),
         ("cu_first", ctypes.c_int32),
+        ("idle_ms", ctypes.c_double),        # ABI 5
+        ("idle_gaps", ctypes.c_uint64),
+        ("affinity_checks", ctypes.c_uint64),
+        ("affinity_failures", ctypes.c_uint64),
     ]
 
 
@@ -96,6 +100,10 @@ class SearchInfo(ctypes.Structure):
         ("overshoot_nonces", ctypes.c_uint64),
         ("late_nonces_losers", ctypes.c_uint64),  # ABI 4: counted on the devices
         ("late_nonces_winner", ctypes.c_uint64),
+        ("adopt_us", ctypes.c_double),            # ABI 5: host timeline
+        ("launch_us", ctypes.c_double),
+        ("launch_all_us", ctypes.c_double),
+        ("win_seen_us", ctypes.c_double),
     ]
 
 
@@ -313,8 +321,9 @@ class Engine:
 
     def __init__(self, path: str = LIB_PATH, cpu_threads: int = 0) -> None:
         """cpu_threads > 0: add that many CPU worker threads as one more logical device after the GPUs
-        (npow_config_cpu_threads; the reference work server's --cpu-threads).  It only takes effect in
-        the process's first Engine (npow_init is process-wide)."""
+        (npow_config_cpu_threads; the reference work server's --cpu-threads).  npow_init is process-wide:
+        asking for CPU threads once the engine is initialised in this process raises NanoPowError
+        (NPOW_ERR_BAD_ARGUMENT), as npow_config_cpu_threads must precede npow_init."""
         self.lib = load(path)
         if cpu_threads:
             _check(self.lib.npow_config_cpu_threads(cpu_threads), self.lib)

@@ -306,9 +306,11 @@ class WorkServer:
             # the reply as soon as the outcome is known (the reference answers when its result validates,
             # nano-work-server.exe @1669040), before a split search's other devices have stopped; the
             # ticket is collected after the reply (_reap)
-            res = t.wait_result() if early else t.wait()
-            if early:
-                self._reap(t)
+            try:
+                res = t.wait_result() if early else t.wait()
+            finally:
+                if early:  # collected even when the outcome is an error (else the engine keeps the job)
+                    self._reap(t)
             if res is not None and res.status == NPOW_OK:
                 log.info("Generated for %s in %.0fms for difficulty %016x", job.root.hex().upper(),
                          (time.perf_counter() - job.t_started) * 1000.0, job.threshold)

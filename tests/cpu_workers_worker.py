@@ -47,6 +47,24 @@ def main():
     r = eng.search(bytes(32), M64, start=12345, device_mask=cmask, max_nonces_per_device=100_003)
     assert r.status == _lib.NPOW_EXHAUSTED and r.nonces_done == 100_003, r
     assert eng.stats(cpu).nonces == 100_003
+    # 2b. a bounded search over all devices (mask 0) leaves the CPU workers out: the GPUs exhaust
+    #     their ranges alone, at GPU speed; naming the CPU device explicitly still includes it (and takes far longer)
+    n_b = 1 << 20
+    t_gpu, t_all = [], []
+    for i in range(3):
+        before = eng.stats(cpu).launches
+        t0 = time.perf_counter()
+        r = eng.search(bytes(32), M64, start=i << 50, device_mask=0, max_nonces_per_device=n_b)
+        t_gpu.append(time.perf_counter() - t0)
+        assert r.status == _lib.NPOW_EXHAUSTED and r.nonces_done == (G - 1) * n_b, r
+        assert eng.stats(cpu).launches == before, "a bounded mask-0 search used the CPU device"
+        t0 = time.perf_counter()
+        r = eng.search(bytes(32), M64, start=i << 50, device_mask=(1 << G) - 1, max_nonces_per_device=n_b)
+        t_all.append(time.perf_counter() - t0)
+        assert r.status == _lib.NPOW_EXHAUSTED and r.nonces_done == G * n_b, r
+    out["bounded_exhaust_ms"] = {"mask0_gpus_only": round(statistics.median(t_gpu) * 1e3, 3),
+                                 "with_cpu_device": round(statistics.median(t_all) * 1e3, 3)}
+    assert statistics.median(t_gpu) < statistics.median(t_all), out
     # 3. a range smaller than one claim is hashed in order by one thread: the first hit is returned
     root = bytes(range(40, 72))
     start = 1 << 50
@@ -65,8 +83,8 @@ def main():
     gpu_best = max(max(oracle.work_values([root] * n, [(base + k * spacing + i) & M64 for i in range(n)]))
                    for k in range(G - 1))
     assert gpu_best < thr
-    t = eng.submit(root, thr, start=base, device_mask=0, max_nonces_per_device=n)
-    info = t.wait_info(60)
+    t = eng.submit(root, thr, start=base, device_mask=(1 << G) - 1, max_nonces_per_device=n)  # (mask 0 would
+    info = t.wait_info(60)                                           # leave the CPU out of a bounded search: 2b)
     assert info.status == _lib.NPOW_OK and info.winner_device == cpu, (info.status, info.winner_device)
     assert info.nonce == (base + cpu * spacing + best) & M64 and info.value == thr
     # 5. GPU + CPU at receive difficulty: valid work; the CPU device takes part; GPU-won jobs are not

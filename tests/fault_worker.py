@@ -18,6 +18,16 @@ work 3 consecutive times" and re-validates every GPU result on the CPU
             search has no device left (NPOW_ERR_NO_DEVICE).
   init      NANOPOW_FAULT_INIT=2, 4 devices: npow_init fails while opening device 2; a retry
             (hook removed) opens all 4 cleanly.
+  cpu_last  NANOPOW_FAULT_HIP=0:0 and NANOPOW_TEST_CPU_RELEASE_DELAY_US, 1 GPU + 4 CPU worker threads:
+            a bounded job over the GPU and the CPU device while a sweep holds the GPU; the CPU device hashes
+            its range and its coordinator is held before it looks at the job; the GPU's first pool launch
+            then fails, and its whole range goes to the CPU device, the only survivor.  The job must end
+            EXHAUSTED with every nonce of both ranges hashed (nonces_done = 2 x the range), not released
+            with the GPU's range unhashed.
+  affinity  NANOPOW_TEST_AFFINITY_SKEW=1, 2 devices: device 1's pool worker finds its thread on the "wrong" HIP
+            device at its first HIP call (the check's failure path, which a one-GPU box cannot reach otherwise):
+            the call fails, device 1 is dropped, every search is still valid on device 0, and every HIP call
+            site of device 0 was checked and found right.
   hooks_off NANOPOW_FAULT_INVALID=0,1 and NANOPOW_FAULT_INIT=0 WITHOUT NANOPOW_TEST_HOOKS=1, 2 devices:
             the hooks are ignored (a stray variable in a deployment must not drop GPUs): init
             succeeds, every search is valid, no device is dropped or counts an invalid result.
@@ -173,8 +183,45 @@ def scenario_hooks_off(eng, G):
     return {"searches": 24}
 
 
+def scenario_cpu_last():
+    import threading
+    import time
+    eng = _lib.Engine(cpu_threads=4)
+    assert eng.n_devices == 2 and eng.cpu_device == 1, (eng.n_devices, eng.cpu_device)
+    n = 1 << 20
+    holder = threading.Thread(target=lambda: eng.sweep(bytes(range(32)), M64, 0, 1 << 34, device_mask=1))
+    holder.start()  # the GPU is busy with a ~0.5-s sweep: the pool's GPU worker cannot launch meanwhile
+    time.sleep(0.05)
+    t0 = time.perf_counter()
+    r = eng.search(bytes(range(5, 37)), M64, start=1 << 44, device_mask=0b11, max_nonces_per_device=n)
+    dt = time.perf_counter() - t0
+    holder.join()
+    assert eng.stats(0).dead == 1, "the GPU's injected launch failure did not drop it"
+    assert r.status == _lib.NPOW_EXHAUSTED and r.nonces_done == 2 * n, (r, 2 * n)
+    assert eng.stats(1).nonces == 2 * n, eng.stats(1).nonces  # both ranges hashed on the CPU device, counted as hashed
+    return {"nonces_done": r.nonces_done, "seconds": round(dt, 3), "devices": 2}
+
+
+def scenario_affinity(eng, G):
+    rng = random.Random(31)
+    for _ in range(24):
+        root = bytes(rng.getrandbits(8) for _ in range(32))
+        r = eng.search(root, RECEIVE, start=rng.getrandbits(64), device_mask=0)
+        assert valid(root, r, RECEIVE), r
+    s0, s1 = eng.stats(0), eng.stats(1)
+    assert s1.dead == 1 and s1.affinity_failures >= 1, (s1.dead, s1.affinity_failures)
+    assert s0.dead == 0 and s0.affinity_checks > 0 and s0.affinity_failures == 0, (s0.affinity_checks,
+                                                                                s0.affinity_failures)
+    return {"device0_checks": s0.affinity_checks, "device1_failures": s1.affinity_failures}
+
+
 def main():
     which = sys.argv[1]
+    if which == "cpu_last":
+        out = scenario_cpu_last()
+        out.update({"scenario": which, "ok": True})
+        print(json.dumps(out), flush=True)
+        return
     if which == "init":
         out = scenario_init()
         out.update({"scenario": which, "devices": 4, "ok": True})
@@ -184,7 +231,7 @@ def main():
     G = eng.n_devices
     assert G == int(os.environ["NANOPOW_VIRTUAL_DEVICES"]), G
     fn = {"invalid": scenario_invalid, "hip": scenario_hip, "exhaust": scenario_exhaust,
-          "allbad": scenario_allbad, "hooks_off": scenario_hooks_off}[which]
+          "allbad": scenario_allbad, "hooks_off": scenario_hooks_off, "affinity": scenario_affinity}[which]
     out = fn(eng, G)
     out.update({"scenario": which, "devices": G, "ok": True})
     print(json.dumps(out), flush=True)

@@ -56,6 +56,8 @@ def main():
         burst(eng, G)
         out["launches_per_device"] = [eng.stats(d).launches for d in range(G)]
         assert all(x > 0 for x in out["launches_per_device"]), out
+        out["affinity"] = [sum(eng.stats(d).affinity_checks for d in range(G)),
+                           sum(eng.stats(d).affinity_failures for d in range(G))]
         out["ok"] = True
         print(json.dumps(out), flush=True)
         return
@@ -123,6 +125,8 @@ def main():
     assert r.status == _lib.NPOW_OK
     used = [eng.stats(d).launches > 0 for d in range(G)]
     assert used == [False, True, False, True], used
+    out["affinity"] = [sum(eng.stats(d).affinity_checks for d in range(G)),
+                       sum(eng.stats(d).affinity_failures for d in range(G))]
     out["ok"] = True
     print(json.dumps(out), flush=True)
 

@@ -55,6 +55,11 @@ def main(n_search, which):
         winners.append(info.winner_device)
     st = [eng.stats(d) for d in range(G)]
     kills = sum(x.kills_relayed for x in st)
+    # the losers' late hashes are deterministic: in each losing device's one-entry launch every workgroup but the
+    # one whose poll read the kill word sees the relayed dead word before a hash and leaves after it -- one hash of
+    # 512 lanes (npow_kernel.hip pool_body_ls2, kind 1) -- while the relaying workgroup leaves at once (kind 2)
+    grid = st[0].grid
+    late_expected = (G - 1) * (grid - 1) * 512 if all(x.grid == grid for x in st) else None
     res = {"ok": True, "devices": G, "threshold": which, "searches": n_search,
            "partitions": [[x.hip_device, x.cu_first, x.cus] for x in st],
            "stop_after_decide_us": {"p50": round(pct(spans, 50), 1), "p99": round(pct(spans, 99), 1),
@@ -65,6 +70,10 @@ def main(n_search, which):
            "late_nonces_losers": {"p50": pct(late_l, 50), "p99": pct(late_l, 99),
                                   "mean_over_nonces_done": round(sum(late_l) / max(1, sum(done)), 5)},
            "late_nonces_winner": {"p50": pct(late_w, 50), "p99": pct(late_w, 99)},
+           "late_expected": late_expected, "grid_per_device": grid,
+           "late_equal_share": round(sum(1 for x in late_l if x == late_expected) / len(late_l), 4),
+           "late_max": max(late_l),
+           "affinity": [sum(x.affinity_checks for x in st), sum(x.affinity_failures for x in st)],
            "finish_ms_p50": round(pct(ttw, 50) / 1e3, 3),
            "result_ms_p50": round(pct(res_ms, 50), 3),
            "distinct_winners": len(set(winners)), "kills_relayed": kills,

@@ -44,7 +44,9 @@ def main():
                       "partitions": [[eng.stats(d).hip_device, eng.stats(d).cu_first, eng.stats(d).cus]
                                      for d in range(G)],
                       "gnps": round(count / dt / 1e9, 3), "nonces_per_device": per,
-                      "hits_per_device": per_dev_hits}), flush=True)
+                      "hits_per_device": per_dev_hits,
+                      "affinity": [sum(eng.stats(d).affinity_checks for d in range(G)),
+                                   sum(eng.stats(d).affinity_failures for d in range(G))]}), flush=True)
 
 
 if __name__ == "__main__":

@@ -21,6 +21,9 @@ SCENARIOS = {
     "allbad": {"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_FAULT_INVALID": "0,1", "NANOPOW_TEST_HOOKS": "1"},
     "init": {"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_FAULT_INIT": "2", "NANOPOW_TEST_HOOKS": "1"},
     "hooks_off": {"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_FAULT_INVALID": "0,1", "NANOPOW_FAULT_INIT": "0"},
+    "cpu_last": {"NANOPOW_VIRTUAL_DEVICES": "1", "NANOPOW_FAULT_HIP": "0:0", "NANOPOW_TEST_HOOKS": "1",
+                 "NANOPOW_TEST_CPU_RELEASE_DELAY_US": "1500000"},
+    "affinity": {"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_TEST_AFFINITY_SKEW": "1", "NANOPOW_TEST_HOOKS": "1"},
 }
 
 

@@ -42,7 +42,10 @@ def bounds(g):
 
 
 def _child(script, env_extra, *args, timeout=110):
-    env = dict(os.environ)
+    """Run a worker with the engine's test hooks on: every HIP call site of every device checks that
+    the calling thread's current HIP device is the device's own (npow_device_stats.affinity_checks); the worker
+    reports the checks and failures, which must be > 0 and 0."""
+    env = dict(os.environ, NANOPOW_TEST_HOOKS="1")
     for k, v in env_extra.items():
         if v is None:
             env.pop(k, None)
@@ -53,6 +56,8 @@ def _child(script, env_extra, *args, timeout=110):
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
     out = json.loads(p.stdout.strip().splitlines()[-1])
     print(json.dumps(out))
+    checks, failures = out["affinity"]
+    assert checks > 0 and failures == 0, out["affinity"]
     return out
 
 

@@ -29,7 +29,7 @@ def _run(binary, env_extra):
 
 @pytest.mark.gpu
 def test_c_abi_under_address_sanitizer():
-    _run("abi_asan_driver", {"ASAN_OPTIONS": "detect_leaks=1:halt_on_error=1",
+    _run("abi_asan_driver", {"ASAN_OPTIONS": "detect_leaks=1:halt_on_error=1:verify_asan_link_order=0",
                              "LSAN_OPTIONS": "suppressions=tools/lsan.supp"})
 
 
@@ -60,7 +60,7 @@ def test_device_drop_under_sanitizers(binary):
     ticket and bounded range over all devices (DRIVER_MASK=0)."""
     env = {"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_FAULT_INVALID": "1", "NANOPOW_TEST_HOOKS": "1", "DRIVER_MASK": "0"}
     if binary == "abi_asan_driver":
-        env.update(ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", LSAN_OPTIONS="suppressions=tools/lsan.supp")
+        env.update(ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:verify_asan_link_order=0", LSAN_OPTIONS="suppressions=tools/lsan.supp")
     else:
         env.update(TSAN_OPTIONS="suppressions=tools/tsan.supp:halt_on_error=1")
     _run(binary, env)
@@ -74,7 +74,7 @@ def test_cpu_workers_under_sanitizers(binary):
     (DRIVER_MASK=0)."""
     env = {"DRIVER_CPU_THREADS": "2", "DRIVER_MASK": "0"}
     if binary == "abi_asan_driver":
-        env.update(ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", LSAN_OPTIONS="suppressions=tools/lsan.supp")
+        env.update(ASAN_OPTIONS="detect_leaks=1:halt_on_error=1:verify_asan_link_order=0", LSAN_OPTIONS="suppressions=tools/lsan.supp")
     else:
         env.update(TSAN_OPTIONS="suppressions=tools/tsan.supp:halt_on_error=1")
     _run(binary, env)

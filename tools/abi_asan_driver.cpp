@@ -47,6 +47,9 @@ static const uint64_t g_mask = [] {
   const char* e = std::getenv("DRIVER_MASK");
   return e ? std::strtoull(e, nullptr, 0) : 1ull;
 }();
+// The bounded ranges name every device explicitly when DRIVER_MASK is 0: mask 0 leaves the CPU workers out of a
+// bounded search (npow_pool.cpp pool_submit), and these runs are to cover them too.  Set in main() after npow_init.
+static uint64_t g_bounded_mask = 1;
 
 // first-win searches at an easy threshold, re-validated on the CPU
 static void searches(int tid, int n) {
@@ -107,7 +110,7 @@ static void sweeps(int tid, int n) {
       CHECK(out[k] == ref[k], "sweep hit %llu", (unsigned long long)k);
 
     uint64_t nonce = 0, value = 0, done = 0;
-    rc = npow_search(root, ~uint64_t(0), start, g_mask, 4096 + i, nullptr, &nonce, &value, &done);
+    rc = npow_search(root, ~uint64_t(0), start, g_bounded_mask, 4096 + i, nullptr, &nonce, &value, &done);
     CHECK(rc == NPOW_EXHAUSTED || rc == NPOW_OK, "bounded rc %d", rc);
     if (rc == NPOW_EXHAUSTED) g_exhausted++;
   }
@@ -130,6 +133,7 @@ int main() {
     return 2;
   }
   std::printf("%s, %d device(s)\n", npow_version(), n_dev);
+  g_bounded_mask = g_mask ? g_mask : (n_dev >= 64 ? ~0ull : (1ull << n_dev) - 1);
 
   // value paths against the CPU
   {

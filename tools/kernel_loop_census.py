@@ -72,6 +72,7 @@ def main():
     ap.add_argument("--kernel", default="npow_pool_kernel_ls2_arg<false>")
     ap.add_argument("--lib", default=os.path.join(ROOT, "nano-dpow_amd", "nanopow", "libnanopow.so"))
     ap.add_argument("--json", action="store_true")
+    ap.add_argument("--dump", action="store_true", help="print the loop's instructions besides the hash stream")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory() as tmp:
         name, base, insts = disassemble(code_object(a.lib, tmp), a.kernel)
@@ -102,6 +103,12 @@ def main():
            "non_stream_valu": sorted(((o, c) for o, c in valu_ops.items()
                                       if o not in ("v_xor_b32_e64", "v_xor_b32", "v_xor_b32_e32", "v_alignbit_b32",
                                                    "v_lshl_add_u64", "v_bitop3_b32")), key=lambda x: -x[1])}
+    if a.dump:
+        stream_ops = ("v_xor_b32_e64", "v_xor_b32", "v_xor_b32_e32", "v_alignbit_b32", "v_lshl_add_u64",
+                      "v_bitop3_b32", "s_setprio")
+        for k, (ad, op, args) in enumerate(body):
+            if op not in stream_ops:
+                print(f"{k:5d} {ad - base:#07x} {op} {args}")
     if a.json:
         print(json.dumps(res))
     else:
