@@ -1226,6 +1226,7 @@ def steady_state(lat, leg, sampler, n):
             "frac_at_measured_sclk": round(achieved / (256 * 128 * mhz * 1e6 / 1e12), 4) if achieved and mhz else None,
             "power_w": pw,
             "cycles_per_hash": round(1024 * 64 * mhz * 1e6 / (kg * 1e9), 1) if kg and mhz else None,
+            "joules_per_gnonce": round(pw["mean"] / lat["gnps"], 2) if pw and lat.get("gnps") else None,
             "what": f"the {n} time-to-work searches at fffffff8 after the timed region (ttw_c_abi_ms; ~11 s, the card "
                     "at its power-capped steady state): value = their nonces / their wall time (the headline's "
                     "definition), kernel_gnps = the kernels' count / their HIP-event time, frac = kernel rate x "
@@ -1499,6 +1500,36 @@ def workload_regime(eng, args, rank, world, dist):
     return line
 
 
+def regime_child(n_dev: int, m: int, timeout: float = 150.0):
+    """The 8-GPU time regime on this box as a child process (the device set is fixed at npow_init, process-wide):
+    bench.py --workload regime over NANOPOW_VIRTUAL_DEVICES = n_dev CU partitions of GPU 0 when the box has one GPU
+    (the rehearsal), or over the first n_dev GPUs when it has that many.  Its node_ttw_8x_regime record, or an
+    error record; never fails the bench."""
+    import subprocess
+    env = dict(os.environ)
+    cmd = [sys.executable, os.path.abspath(__file__), "--workload", "regime", "--gpus", str(n_dev), "--steps", str(m),
+           "--http-requests", "100"]
+    try:
+        n_phys = int(subprocess.run([sys.executable, "-c", "import ctypes; h = ctypes.CDLL('libamdhip64.so.7'); "
+                                     "n = ctypes.c_int(0); h.hipGetDeviceCount(ctypes.byref(n)); print(n.value)"],
+                                    capture_output=True, text=True, timeout=60).stdout.strip() or 0)
+    except (OSError, ValueError, subprocess.SubprocessError):
+        n_phys = 0
+    if n_phys < n_dev:
+        env["NANOPOW_VIRTUAL_DEVICES"] = str(n_dev)
+    try:
+        p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=timeout)
+        line = json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else None
+    except (OSError, ValueError, IndexError, subprocess.SubprocessError) as e:
+        return {"error": repr(e)[:300]}
+    if line is None:
+        return {"error": f"rc {p.returncode}: {p.stderr[-300:]}"}
+    rec = line["node_ttw_8x_regime"]
+    rec["devices_are"] = (f"{n_dev} CU partitions of GPU 0 (NANOPOW_VIRTUAL_DEVICES, one CU-masked stream each)"
+                          if "NANOPOW_VIRTUAL_DEVICES" in env else f"{n_dev} physical GPUs")
+    return rec
+
+
 def workload_receive(eng, args, rank, world, dist):
     """BASELINE config 1: work_generate at fffffe0000000000, GPU next to the CPU reference."""
     if world > 1:
@@ -1713,6 +1744,9 @@ def main() -> int:
                     help="search, N=1: work_generate requests timed at the JSON boundary after the timed steps")
     ap.add_argument("--latency-searches", type=int, default=1000,
                     help="search, N=1: C-ABI searches on R_0..R_{n-1} after the timed steps (p50/p99 time-to-work)")
+    ap.add_argument("--regime-searches", type=int, default=500,
+                    help="search, N=1: searches of the 8-GPU time regime run in a child process after the bench "
+                         "(node_ttw_8x_regime; 0 = skip)")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("bench.py: --gpus must be >= 1")
@@ -1836,6 +1870,8 @@ def main() -> int:
         if cpu:
             line["cpu_baseline"] = cpu
         line["device_check"] = device_check([g[2] for g in gathered], res[4], res[0])
+        if WORLD == 1 and args.regime_searches:
+            line["node_ttw_8x_regime"] = regime_child(8, args.regime_searches)
         print(json.dumps(line), flush=True)
     rc = 0
     if rank == 0 and not line["device_check"]["ok"]:

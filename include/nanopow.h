@@ -60,8 +60,8 @@ extern "C" {
  * are written up to the size the caller passes, so revision-3 callers are unaffected).
  * 5: npow_search_info gains the search's host timeline (adopt_us, launch_us, launch_all_us, win_seen_us);
  * npow_device_stats gains idle_ms / idle_gaps (the GPU idle between the device's search launches) and
- * affinity_checks / affinity_failures (NANOPOW_TEST_HOOKS=1: the calling thread's HIP device checked at every HIP
- * call site of the device).  Both structs are still written up to the size the caller passes. */
+ * affinity_checks / affinity_failures (NANOPOW_TEST_HOOKS=1, since npow_init: the calling thread's HIP device checked
+ * at every HIP call site of the device) and watcher_decisions.  Both structs are still written up to the size the caller passes. */
 #define NPOW_ABI_VERSION 5
 
 /* Hash paths of npow_values_path. */
@@ -114,6 +114,8 @@ typedef struct npow_device_stats {
   uint64_t affinity_checks; /* NANOPOW_TEST_HOOKS=1: HIP call sites of this device at which the calling thread's
                                current HIP device was checked (hipGetDevice == hip_device) ... */
   uint64_t affinity_failures; /* ... and found wrong (the call then fails: NPOW_ERR_INTERNAL) */
+  uint64_t watcher_decisions; /* jobs decided by the process's win watcher from this device's win records (it spins
+                                 over every live slot's record; NANOPOW_WATCHER=0 leaves them to the device's worker) */
 } npow_device_stats;
 
 /* Outcome of one search (npow_wait_info).  Times are host steady-clock microseconds since

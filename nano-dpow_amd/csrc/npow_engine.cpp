@@ -544,6 +544,7 @@ static int stats_fill(int device, npow_device_stats* out) {
   out->idle_gaps = d.idle_gaps;
   out->affinity_checks = d.affinity_checks.load(std::memory_order_relaxed);
   out->affinity_failures = d.affinity_failures.load(std::memory_order_relaxed);
+  out->watcher_decisions = d.watcher_decisions;
   return NPOW_OK;
 }
 
@@ -572,7 +573,7 @@ int npow_device_stats_reset(int device) try {
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
   d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = d.kills_relayed = d.late = 0;
-  d.idle_gaps = 0;
+  d.idle_gaps = d.watcher_decisions = 0;
   d.idle_ms = 0.0;
   d.kernel_ms = 0.0;
   d.clk_ticks = d.clk_ref_ticks = 0.0;

@@ -5,6 +5,7 @@
 #include <pthread.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <chrono>
 #include <memory>
 #include <mutex>
@@ -64,6 +65,7 @@ struct Device {
   uint64_t yields = 0, dyn = 0;            // launches yielded / jobs that joined a running launch
   uint64_t kills_relayed = 0;              // losing jobs stopped by another device's decision (npow_pool.cpp)
   uint64_t late = 0;                       // device-side overshoot: nonces hashed after the job was known over
+  uint64_t watcher_decisions = 0;          // jobs the win watcher decided from this device's win records
   double idle_ms = 0.0;                    // GPU idle between consecutive search launches (HIP events) ...
   uint64_t idle_gaps = 0;                  // ... over this many pairs (npow_pool.cpp Worker::retire)
   // Published by the pool worker for npow_device_stats_get: it has launches or slots in flight, and
@@ -71,6 +73,20 @@ struct Device {
   // held it is retired; with no slot searching, the stats wait for the worker to retire the rest.
   std::atomic<bool> worker_busy{false};
   std::atomic<int> active_slots{0};
+  // The pool worker naps between steps on its own condition variable (round 5; it napped on g_pool.cv_work with
+  // g_pool.mu, and every admission or decision then woke all the workers into a convoy on that lock): new jobs,
+  // decisions and shutdown bump wake_seq (under wake_mu) and notify.
+  std::mutex wake_mu;
+  std::condition_variable wake_cv;
+  uint64_t wake_seq = 0;
+  // The win watcher (npow_pool.cpp watcher_run): the slots whose win records it watches, armed by the pool worker
+  // when it adopts a job (bit s of armed_mask, the generation in armed_gen[s], the job in armed_job[s] under
+  // armed_mu) and disarmed when the slot is freed.
+  std::atomic<uint64_t> armed_mask{0};
+  std::atomic<uint64_t> armed_gen[kMaxSlots] = {};
+  std::atomic<const volatile uint32_t*> armed_cancel[kMaxSlots] = {};  // the job's caller-owned cancel word, if any
+  std::mutex armed_mu;
+  std::shared_ptr<void> armed_job[kMaxSlots];  // JobP (npow_pool.h), type-erased here
   double kernel_ms = 0.0;
   double clk_ticks = 0.0, clk_ref_ticks = 0.0;  // in-kernel s_memtime / s_memrealtime spans (stats)
   std::chrono::steady_clock::time_point stats_t0 = std::chrono::steady_clock::now();

@@ -82,6 +82,11 @@ const double g_poll_us = [] {
   return e ? atof(e) : 50.0;
 }();
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
+// The win watcher (watcher_run): on by default; NANOPOW_WATCHER=0 turns it off (A/B runs)
+const bool g_watcher_on = [] {
+  const char* e = getenv("NANOPOW_WATCHER");
+  return !(e && strcmp(e, "0") == 0);
+}();
 const bool g_trace_lat = getenv("NANOPOW_TRACE_LATENCY") != nullptr;
 // NANOPOW_TRACE_STEPS=1: each pool worker times the parts of its steps (adopt, check_slots, read-back, launch, retire,
 // nap) and prints count / total / max / calls over 50 us per part when it exits (diagnostics of the host path)
@@ -147,13 +152,30 @@ std::atomic<uint64_t> g_gen{0};
 std::atomic<bool> g_exiting{false};  // process exit: workers leave at once, no further HIP calls
 
 // -- job state transitions (caller holds g_pool.mu) ------------------------------------------
+static void notify_waiters(Job& j) {
+  { std::lock_guard<std::mutex> g(j.wmu); }  // a waiter between its check and its wait cannot miss the notify
+  j.cv.notify_all();
+}
+
+void notify_workers_locked() {
+  g_pool.cv_work.notify_all();
+  for (auto& dp : g_devs) {
+    Device& d = *dp;
+    {
+      std::lock_guard<std::mutex> g(d.wake_mu);
+      ++d.wake_seq;
+    }
+    d.wake_cv.notify_one();
+  }
+}
+
 void decide_locked(Job& j, int status, uint64_t nonce, uint64_t value) {
   if (j.status != kPending) return;
   j.status = status;
   j.nonce = nonce;
   j.value = value;
-  j.decided = true;
-  j.cv.notify_all();  // npow_wait_result returns at the decision
+  j.decided.store(true, std::memory_order_release);  // the outcome above is read by waiters that acquire this
+  notify_waiters(j);  // npow_wait_result returns at the decision
 }
 
 void admit_locked() {
@@ -167,7 +189,7 @@ void admit_locked() {
   }
   if (added) {
     g_pool.version.fetch_add(1);
-    g_pool.cv_work.notify_all();
+    notify_workers_locked();
   }
 }
 
@@ -180,13 +202,13 @@ void finish_locked(const JobP& j) {
     j->decided = true;
   }
   j->t_finish = now_us();
-  j->finished = true;
+  j->finished.store(true, std::memory_order_release);
   auto it = std::find(g_pool.active.begin(), g_pool.active.end(), j);
   if (it != g_pool.active.end()) g_pool.active.erase(it);
   auto wt = std::find(g_pool.waiting.begin(), g_pool.waiting.end(), j);
   if (wt != g_pool.waiting.end()) g_pool.waiting.erase(wt);
   admit_locked();
-  j->cv.notify_all();
+  notify_waiters(*j);
 }
 
 // Device k of job j is finished with it (retired, exhausted, or the device failed).
@@ -233,7 +255,7 @@ void abandon_locked(const JobP& j, size_t k, int code, const std::string& msg) {
           ++j->pending_devs;
         }
       g_pool.version.fetch_add(1);
-      g_pool.cv_work.notify_all();
+      notify_workers_locked();
     }
   }
   device_done_locked(j, k);
@@ -257,7 +279,7 @@ void stop_other_devices_locked(Job& j, size_t k_win) {
     d.kills_relayed++;
   }
   g_pool.decisions.fetch_add(1, std::memory_order_release);
-  g_pool.cv_work.notify_all();
+  notify_workers_locked();
 }
 
 int index_in(const Job& j, int dev) {
@@ -274,6 +296,140 @@ bool wants_device_locked(int dev) {
   }
   return false;
 }
+
+// -- the win watcher ------------------------------------------------------------------------------
+// A device's pool worker sees its winner records only between its naps (up to g_poll_us = 50 us once a launch is
+// 0.4 ms old), and over 8 devices a worker woken by a notify queues for the pool lock behind the others.  One thread
+// for the whole process instead spins over the win records of every armed slot of every GPU while any job is live
+// (one core; it reads pinned host memory only, no HIP call), re-validates a winner on the CPU and decides the job
+// at once: the result goes to the client and the other devices' kill words go up within microseconds of the
+// record landing.  The winner's worker handles the same record at its next step as before (an invalid result, the
+// device's invalid streak and the slot's retirement stay its business; a job already decided is left alone).
+// It also watches each armed job's cancel word (a caller's work_cancel, or another rank's first win through a shared
+// word, bench.py node_time_to_work) and wakes the device's worker at once, which then stops the job's waves.
+namespace {
+struct Watch {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<int> armed{0};  // armed slots over all devices
+  bool stop = false;
+  std::thread th;
+};
+Watch g_watch;
+}  // namespace
+
+void watch_arm(Device& d, int s, uint64_t gen, const JobP& j) {
+  if (!g_watcher_on) return;
+  {
+    std::lock_guard<std::mutex> g(d.armed_mu);
+    d.armed_job[s] = j;
+  }
+  d.armed_cancel[s].store(j->cancel, std::memory_order_release);
+  d.armed_gen[s].store(gen, std::memory_order_release);
+  const uint64_t bit = 1ull << s;
+  if (!(d.armed_mask.fetch_or(bit, std::memory_order_acq_rel) & bit) &&
+      g_watch.armed.fetch_add(1, std::memory_order_acq_rel) == 0) {
+    { std::lock_guard<std::mutex> g(g_watch.mu); }
+    g_watch.cv.notify_one();
+  }
+}
+
+void watch_disarm(Device& d, int s) {
+  if (!g_watcher_on) return;
+  const uint64_t bit = 1ull << s;
+  if (d.armed_mask.fetch_and(~bit, std::memory_order_acq_rel) & bit) g_watch.armed.fetch_sub(1, std::memory_order_acq_rel);
+  std::lock_guard<std::mutex> g(d.armed_mu);  // (see watch_stop_cancel)
+  d.armed_gen[s].store(0, std::memory_order_release);
+  d.armed_cancel[s].store(nullptr, std::memory_order_release);
+  d.armed_job[s].reset();
+}
+
+// The slot leaves the searching state: the watcher stops reading its job's cancel word.  Under armed_mu, which the
+// watcher holds while it reads the word: the device cannot finish with the job before this, so the job cannot end and
+// its caller free the word while the watcher reads it.
+void watch_stop_cancel(Device& d, int s) {
+  if (!g_watcher_on) return;
+  std::lock_guard<std::mutex> g(d.armed_mu);
+  d.armed_cancel[s].store(nullptr, std::memory_order_release);
+}
+
+static void wake_worker(Device& d) {
+  {
+    std::lock_guard<std::mutex> g(d.wake_mu);
+    ++d.wake_seq;
+  }
+  d.wake_cv.notify_one();
+}
+
+namespace {
+void watch_handle(Device& d, int s, uint64_t gen) {
+  const double t_seen = now_us();
+  JobP j;
+  {
+    std::lock_guard<std::mutex> g(d.armed_mu);
+    if (d.armed_gen[s].load(std::memory_order_acquire) == gen) j = std::static_pointer_cast<Job>(d.armed_job[s]);
+  }
+  if (!j) return;
+  const PoolWin& pw = d.pmb->win[s];
+  const uint64_t n = __atomic_load_n(&pw.nonce, __ATOMIC_RELAXED);
+  uint64_t v = __atomic_load_n(&pw.value, __ATOMIC_RELAXED);
+  if (__atomic_load_n(&pw.gen, __ATOMIC_ACQUIRE) != gen) return;  // the record moved on meanwhile
+  if ((faults().invalid_mask >> d.id) & 1) v ^= 1;                 // NANOPOW_FAULT_INVALID (tests)
+  if (host_work_value(j->pre.m, n) != v || v < j->threshold) return;  // invalid: the worker's business
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  const int k = index_in(*j, d.id);
+  if (j->status != kPending || k < 0 || j->dev_gen[(size_t)k] != gen) return;
+  decide_locked(*j, NPOW_OK, n, v);
+  j->t_decide = now_us();
+  j->t_win_seen = t_seen;
+  if (j->t_win == 0) j->t_win = t_seen;
+  j->winner_k = k;
+  stop_other_devices_locked(*j, (size_t)k);
+  if (j->devs.size() < 2) notify_workers_locked();  // (stop_other_devices_locked wakes them for split jobs)
+  std::lock_guard<std::mutex> sg(d.stats_mu);
+  d.watcher_decisions++;
+}
+
+void watcher_run() {
+  prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+  std::vector<std::vector<uint64_t>> handled(g_devs.size(), std::vector<uint64_t>(kMaxSlots, 0));
+  std::vector<std::vector<uint64_t>> cancelled(g_devs.size(), std::vector<uint64_t>(kMaxSlots, 0));
+  for (;;) {
+    if (g_watch.armed.load(std::memory_order_acquire) == 0) {
+      std::unique_lock<std::mutex> lk(g_watch.mu);
+      g_watch.cv.wait(lk, [] { return g_watch.stop || g_watch.armed.load(std::memory_order_acquire) > 0; });
+      if (g_watch.stop) return;
+    }
+    if (g_exiting.load(std::memory_order_relaxed)) return;
+    for (size_t di = 0; di < g_devs.size(); ++di) {
+      Device& d = *g_devs[di];
+      uint64_t m = d.armed_mask.load(std::memory_order_acquire);
+      while (m) {
+        const int s = __builtin_ctzll(m);
+        m &= m - 1;
+        const uint64_t gen = d.armed_gen[s].load(std::memory_order_acquire);
+        if (gen && gen != handled[di][s] && __atomic_load_n(&d.pmb->win[s].gen, __ATOMIC_ACQUIRE) == gen) {
+          handled[di][s] = gen;
+          watch_handle(d, s, gen);
+        }
+        if (gen && gen != cancelled[di][s] && d.armed_cancel[s].load(std::memory_order_acquire)) {
+          bool raised;
+          {
+            std::lock_guard<std::mutex> g(d.armed_mu);  // (watch_stop_cancel)
+            const volatile uint32_t* c = d.armed_cancel[s].load(std::memory_order_acquire);
+            raised = c && load_acquire(c);
+          }
+          if (raised) {
+            cancelled[di][s] = gen;
+            wake_worker(d);  // its check_slots sees the cancel word and raises the slot's kill word
+          }
+        }
+      }
+    }
+    cpu_relax();
+  }
+}
+}  // namespace
 
 namespace {
 
@@ -329,6 +485,7 @@ class Worker {
   std::chrono::steady_clock::time_point front_start_{};  // host estimate of the running launch's start
   uint64_t yields_ = 0;
   uint64_t ctl_ = 0;  // PoolMailbox::ctl (only this worker writes it): yields << 32 | dynamic entries
+  uint64_t wake_seen_ = 0;  // Device::wake_seq as of this worker's last nap
   int invalid_streak_ = 0;  // consecutive winners of this device that failed CPU re-validation
   int prev_stop_ring_ = -1;  // ring of the last retired launch (its stop event: the GPU idle before the next one),
                              // -1 when a sweep / values task used the device's events since
@@ -423,6 +580,7 @@ void Worker::adopt() {
     j->on_dev[k] = 1;
     j->dev_slot[k] = s;
     j->dev_gen[k] = sl.gen;
+    watch_arm(d_, s, sl.gen, j);
     if (j->t_adopt == 0) j->t_adopt = now_us();
     sl.new_job = !j->seen_dev[k];
     if (sl.new_job) adopted = true;  // a new job: worth ending a long launch for
@@ -515,6 +673,7 @@ void Worker::yield_if_long() {
     if (sl.state != SlotState::kActive || sl.fresh || sl.job->max_per_dev) continue;
     sl.requeue = true;
     sl.state = SlotState::kDraining;
+    watch_stop_cancel(d_, (int)(&sl - slots_));
     any = true;
   }
   NPOW_DBG("nanopow[%d]: yield %s\n", d_.id, any ? "raised" : "(no slot to hand back)");
@@ -578,6 +737,7 @@ void Worker::handle_win(int s) {
     }
   }
   sl.state = SlotState::kDraining;  // the winning wave already marked the slot dead on the device
+  watch_stop_cancel(d_, (int)(&sl - slots_));
   sl.stop_us = now_us();
 }
 
@@ -698,6 +858,7 @@ void Worker::check_slots() {
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);
       __atomic_fetch_add(&d_.pmb->kills, 1ull, __ATOMIC_RELEASE);
       sl.state = SlotState::kDraining;
+      watch_stop_cancel(d_, (int)(&sl - slots_));
     } else if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {
       {
         std::lock_guard<std::mutex> g(g_pool.mu);
@@ -715,9 +876,11 @@ void Worker::check_slots() {
       __atomic_store_n(&d_.pmb->kill[s], sl.gen, __ATOMIC_RELEASE);  // in-flight waves stop
       __atomic_fetch_add(&d_.pmb->kills, 1ull, __ATOMIC_RELEASE);
       sl.state = SlotState::kDraining;
+      watch_stop_cancel(d_, (int)(&sl - slots_));
       sl.stop_us = now_us();
     } else if (sl.no_more) {
       sl.state = SlotState::kDraining;
+      watch_stop_cancel(d_, (int)(&sl - slots_));
     }
   }
   publish_busy();  // before a job can finish early: its waiter may read the stats at once
@@ -942,6 +1105,7 @@ int Worker::retire() {
         device_done_locked(sl.job, sl.k);
       }
     }
+    watch_disarm(d_, s);
     sl.job.reset();
     sl.state = SlotState::kFree;
   }
@@ -970,6 +1134,7 @@ void Worker::fail_all(const std::string& msg) {
       const bool stopped = sl.win_seen || sl.stop_us > 0;
       if (!sl.early) sl.job->done += sl.unread + (stopped ? 0 : kept);
     }
+    watch_disarm(d_, (int)(&sl - slots_));  // before the job can end (abandon_locked): the watcher reads its cancel word
     abandon_locked(sl.job, sl.k, d_.dead_code, d_.dead_msg);
     sl.job.reset();
     sl.inflight.clear();
@@ -1096,13 +1261,12 @@ void Worker::nap() {
     }
     us = std::min(us, until_prelaunch);
   }
-  const uint64_t v = seen_version_;
-  const uint64_t dec = g_pool.decisions.load(std::memory_order_acquire);
-  std::unique_lock<std::mutex> lk(g_pool.mu);
-  g_pool.cv_work.wait_for(lk, std::chrono::duration<double, std::micro>(us), [&] {
-    return g_pool.version.load(std::memory_order_relaxed) != v || !g_pool.running || d_.tasks_waiting.load() > 0 ||
-           g_pool.decisions.load(std::memory_order_relaxed) != dec;
-  });
+  // on the device's own condition variable (round 5): new jobs, decisions and shutdown bump wake_seq
+  // (notify_workers_locked); one that came since the last nap returns at once
+  std::unique_lock<std::mutex> wl(d_.wake_mu);
+  d_.wake_cv.wait_for(wl, std::chrono::duration<double, std::micro>(us),
+                      [&] { return d_.wake_seq != wake_seen_ || d_.tasks_waiting.load() > 0; });
+  wake_seen_ = d_.wake_seq;
 }
 
 }  // namespace
@@ -1155,6 +1319,13 @@ void pool_start() {
     std::lock_guard<std::mutex> g(g_pool.mu);
     g_pool.running = true;
   }
+  if (g_watcher_on) {
+    {
+      std::lock_guard<std::mutex> g(g_watch.mu);
+      g_watch.stop = false;
+    }
+    g_watch.th = std::thread(watcher_run);
+  }
   for (auto& dp : g_devs) {
     Device* d = dp.get();
     if (d->cpu_threads) {
@@ -1178,21 +1349,33 @@ void pool_stop() {
     std::lock_guard<std::mutex> g(g_pool.mu);
     g_pool.running = false;
     for (const JobP& j : g_pool.active) j->cancel_req = true;
-    g_pool.cv_work.notify_all();
+    notify_workers_locked();
   }
   for (auto& d : g_devs)
     if (d->worker.joinable()) d->worker.join();
+  if (g_watch.th.joinable()) {
+    {
+      std::lock_guard<std::mutex> g(g_watch.mu);
+      g_watch.stop = true;
+    }
+    g_watch.cv.notify_all();
+    g_watch.th.join();
+  }
+  for (auto& dp : g_devs)  // a worker that left with slots armed (shutdown): nothing is watched any more
+    for (int s = 0; s < kMaxSlots; ++s) watch_disarm(*dp, s);
   std::lock_guard<std::mutex> g(g_pool.mu);
   for (auto& kv : g_pool.tickets) {
     const JobP& j = kv.second;
     if (!j->finished) {
-      if (j->err.empty()) j->err = "engine shut down";
-      j->status = NPOW_ERR_NOT_INITIALISED;
-      j->decided = true;
-      j->finished = true;
+      if (!j->decided) {  // a decided job keeps its outcome: waiters may read it without the lock
+        j->err = "engine shut down";
+        j->status = NPOW_ERR_NOT_INITIALISED;
+        j->decided.store(true, std::memory_order_release);
+      }
+      j->finished.store(true, std::memory_order_release);
     }
   }
-  for (auto& kv : g_pool.tickets) kv.second->cv.notify_all();
+  for (auto& kv : g_pool.tickets) notify_waiters(*kv.second);
   g_pool.waiting.clear();
   g_pool.active.clear();
 }
@@ -1242,32 +1425,49 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   return NPOW_OK;
 }
 
-int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done,
-              npow_search_info* info) {
-  std::unique_lock<std::mutex> lk(g_pool.mu);
-  auto it = g_pool.tickets.find(ticket);
-  if (it == g_pool.tickets.end()) return fail(NPOW_ERR_BAD_ARGUMENT, "unknown ticket");
-  JobP j = it->second;
+// Wait, without g_pool.mu, until done() holds (NPOW_OK) or the timeout passes (NPOW_PENDING).  A queued job's
+// cancel word is polled here every 2 ms (admitted ones are polled by the device workers), and such a job is cancelled
+// under the pool lock.
+template <class Done>
+static int wait_job(const JobP& j, int64_t timeout_us, Done done) {
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us < 0 ? 0 : timeout_us);
-  while (!j->finished) {
-    // A queued job's cancel word is polled here, every 2 ms (admitted ones are polled by the
-    // device workers, and their waiters sleep until the job's own end).
-    if (!j->admitted && j->cancel_seen()) {
-      j->cancel_req = true;
-      decide_locked(*j, NPOW_CANCELLED);
-      finish_locked(j);
-      break;
+  for (;;) {
+    if (done()) return NPOW_OK;
+    if (!j->admitted.load(std::memory_order_acquire) && j->cancel_seen()) {
+      std::lock_guard<std::mutex> g(g_pool.mu);
+      if (!j->admitted && !j->finished) {
+        j->cancel_req = true;
+        decide_locked(*j, NPOW_CANCELLED);
+        finish_locked(j);
+      }
+      continue;
     }
     const auto now = std::chrono::steady_clock::now();
     if (timeout_us >= 0 && now >= deadline) return NPOW_PENDING;
-    if (j->admitted && timeout_us < 0) {
-      j->cv.wait(lk);
+    std::unique_lock<std::mutex> wl(j->wmu);
+    if (j->admitted.load(std::memory_order_acquire) && timeout_us < 0) {
+      j->cv.wait(wl, done);
     } else {
-      auto wake = j->admitted ? deadline : now + std::chrono::microseconds(2000);
+      auto wake = j->admitted.load(std::memory_order_acquire) ? deadline : now + std::chrono::microseconds(2000);
       if (timeout_us >= 0) wake = std::min(wake, deadline);
-      j->cv.wait_until(lk, wake);
+      j->cv.wait_until(wl, wake, done);
     }
   }
+}
+
+static JobP find_ticket(uint64_t ticket) {
+  std::lock_guard<std::mutex> g(g_pool.mu);
+  auto it = g_pool.tickets.find(ticket);
+  return it == g_pool.tickets.end() ? nullptr : it->second;
+}
+
+int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value, uint64_t* nonces_done,
+              npow_search_info* info) {
+  JobP j = find_ticket(ticket);
+  if (!j) return fail(NPOW_ERR_BAD_ARGUMENT, "unknown ticket");
+  if (wait_job(j, timeout_us, [&] { return j->finished.load(std::memory_order_acquire); }) == NPOW_PENDING)
+    return NPOW_PENDING;
+  std::unique_lock<std::mutex> lk(g_pool.mu);
   if (nonces_done) *nonces_done = j->done;
   if (info) {
     info->winner_device = j->winner_k >= 0 ? j->devs[(size_t)j->winner_k] : -1;
@@ -1330,28 +1530,13 @@ int pool_wait(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* va
 // The search's outcome as soon as it is known (npow_wait_result): the winner accepted or the job cancelled,
 // while the other devices may still be stopping; the ticket stays valid for pool_wait.
 int pool_wait_result(uint64_t ticket, int64_t timeout_us, uint64_t* nonce, uint64_t* value) {
-  std::unique_lock<std::mutex> lk(g_pool.mu);
-  auto it = g_pool.tickets.find(ticket);
-  if (it == g_pool.tickets.end()) return fail(NPOW_ERR_BAD_ARGUMENT, "unknown ticket");
-  JobP j = it->second;
-  const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us < 0 ? 0 : timeout_us);
-  while (j->status == kPending && !j->finished) {
-    if (!j->admitted && j->cancel_seen()) {  // as pool_wait: a queued job's cancel word is polled here
-      j->cancel_req = true;
-      decide_locked(*j, NPOW_CANCELLED);
-      finish_locked(j);
-      break;
-    }
-    const auto now = std::chrono::steady_clock::now();
-    if (timeout_us >= 0 && now >= deadline) return NPOW_PENDING;
-    if (j->admitted && timeout_us < 0) {
-      j->cv.wait(lk);
-    } else {
-      auto wake = j->admitted ? deadline : now + std::chrono::microseconds(2000);
-      if (timeout_us >= 0) wake = std::min(wake, deadline);
-      j->cv.wait_until(lk, wake);
-    }
-  }
+  JobP j = find_ticket(ticket);
+  if (!j) return fail(NPOW_ERR_BAD_ARGUMENT, "unknown ticket");
+  if (wait_job(j, timeout_us, [&] {
+        return j->decided.load(std::memory_order_acquire) || j->finished.load(std::memory_order_acquire);
+      }) == NPOW_PENDING)
+    return NPOW_PENDING;
+  // the outcome was written before `decided` was released, and is never written after it
   const int st = j->status;
   if (st == NPOW_OK) {
     if (nonce) *nonce = j->nonce;
@@ -1372,6 +1557,8 @@ int pool_cancel(uint64_t ticket) {
   if (!j->admitted) {
     decide_locked(*j, NPOW_CANCELLED);
     finish_locked(j);
+  } else {
+    notify_workers_locked();  // the devices' workers stop its waves at their next step, now rather than after a nap
   }
   return NPOW_OK;
 }

@@ -43,12 +43,17 @@ struct Job {
                                     // (device-side count, PoolDevState kLateWord)
   int winner_k = -1;                // the device whose result decided the job
   int pending_devs = 0;
-  bool admitted = false;
+  std::atomic<bool> admitted{false};  // written under g_pool.mu; waiters read it without it
   bool lost = false;                // a dead device's remainder had no surviving device to go to
   int lost_code = NPOW_ERR_HIP;
   std::atomic<bool> finished{false};  // written under g_pool.mu; waiters may spin on it
-  std::condition_variable cv;         // its waiters (pool_wait), notified by finish_locked: one job's end
-                                      // wakes only its own waiters, not every thread blocked in npow_wait
+  // Its waiters (pool_wait, pool_wait_result) sleep on cv with wmu, not g_pool.mu (round 5): a waiter woken at the
+  // decision then returns without queueing for the pool lock behind the workers that the same decision woke (over 8
+  // devices that convoy cost ~25 us per search, profiles/r05a_regime8_new.json).  decide_locked / finish_locked lock
+  // wmu before they notify, and a job's outcome (status, nonce, value, err) is written before `decided` is
+  // released and never after it, so a waiter reads it once it has acquired `decided`.
+  std::mutex wmu;
+  std::condition_variable cv;
   int status = kPending;
   uint64_t nonce = 0, value = 0, done = 0;
   std::string err;
@@ -66,7 +71,7 @@ using JobP = std::shared_ptr<Job>;
 
 struct Pool {
   std::mutex mu;
-  std::condition_variable cv_work;  // workers: new admissions / shutdown
+  std::condition_variable cv_work;  // idle workers: new admissions / shutdown (busy ones nap on their device's wake_cv)
   std::deque<JobP> waiting;
   std::vector<JobP> active;
   std::unordered_map<uint64_t, JobP> tickets;
@@ -89,6 +94,7 @@ void device_done_locked(const JobP& j, size_t k);
 void abandon_locked(const JobP& j, size_t k, int code, const std::string& msg);
 void stop_other_devices_locked(Job& j, size_t k_win);
 int index_in(const Job& j, int dev);  // the job's index of logical device dev, or -1
+void notify_workers_locked();         // wake the idle workers (cv_work) and the napping ones (each device's wake_cv)
 bool wants_device_locked(int dev);    // some active job wants this device
 
 // -- CPU workers (npow_cpu.cpp) ------------------------------------------------------------------

@@ -81,6 +81,7 @@ class DeviceStats(ctypes.Structure):
         ("idle_gaps", ctypes.c_uint64),
         ("affinity_checks", ctypes.c_uint64),
         ("affinity_failures", ctypes.c_uint64),
+        ("watcher_decisions", ctypes.c_uint64),
     ]
 
 

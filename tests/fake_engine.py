@@ -41,7 +41,8 @@ class _Ticket:
         r, info = self._res, self._info
         return info or SimpleNamespace(status=r.status, nonce=r.nonce, value=r.value, nonces_done=r.nonces_done,
                                        winner_device=0, n_devices=1, decide_us=0.0, finish_us=0.0,
-                                       stop_after_decide_us=0.0, overshoot_nonces=0, late_nonces_losers=0, late_nonces_winner=0)
+                                       stop_after_decide_us=0.0, overshoot_nonces=0, late_nonces_losers=0, late_nonces_winner=0,
+                                       adopt_us=0.0, launch_us=0.0, launch_all_us=0.0, win_seen_us=0.0)
 
 
 class OracleEngine:
@@ -62,7 +63,8 @@ class OracleEngine:
         return SimpleNamespace(kernel_ms=st["kernel_ms"], nonces=st["nonces"], launches=st["launches"],
                                clock_mhz=0.0, early_finishes=0, kills_relayed=0, host_cpu_ms=0.0,
                                host_wall_ms=1.0, grid=0, pool_groups=4, late_nonces=0, hip_device=0,
-                               cu_first=-1)
+                               cu_first=-1, cus=256, idle_ms=0.0, idle_gaps=0, affinity_checks=0, affinity_failures=0,
+                               watcher_decisions=0)
 
     def version(self):
         return "oracle stand-in engine (tests/fake_engine.py)"
@@ -107,7 +109,8 @@ class OracleEngine:
         info = SimpleNamespace(status=NPOW_OK, nonce=win.nonce, value=win.value, nonces_done=done,
                                winner_device=devs[k], n_devices=G, decide_us=(td - t0) * 1e6,
                                finish_us=(max(te for _, te in out) - t0) * 1e6,
-                               stop_after_decide_us=max(spans, default=0.0), overshoot_nonces=0, late_nonces_losers=0, late_nonces_winner=0)
+                               stop_after_decide_us=max(spans, default=0.0), overshoot_nonces=0, late_nonces_losers=0, late_nonces_winner=0,
+                               adopt_us=0.0, launch_us=0.0, launch_all_us=0.0, win_seen_us=(td - t0) * 1e6)
         return res, info
 
     def work_value(self, root, nonce):

@@ -204,3 +204,27 @@ def test_inprocess_multi_gpu_path_with_oracle_engine():
         a, b = sorted(v)
         assert (b - a) % (1 << 64) == 1 << 63 or (a - b) % (1 << 64) == 1 << 63
     assert oracle.work_value(root, 0) >= 0  # the checker is importable here
+
+
+def test_regime_harness_with_oracle_engine():
+    """bench.py --workload regime on the oracle stand-in over 2 emulated devices: one root at a time,
+    the next submitted at the previous result, tickets collected by the reaper; the record's rates, expectation and
+    fixed-cost decomposition are filled in, and the device check passes on equal, fully counted devices."""
+    import bench
+    from fake_engine import OracleEngine
+    eng = OracleEngine(chunk=1 << 10, n_devices=2)
+    rec = bench.node_regime(eng, 2, 12, thr=0xfff0000000000000)
+    assert rec["devices"] == 2 and rec["searches"] == 12 and rec["threshold"] == "fff0000000000000"
+    assert rec["c_abi_ttw_ms"]["p99"] >= rec["c_abi_ttw_ms"]["p50"] > 0
+    assert rec["kernel_gnps"] > 0 and rec["node_gnps"] > 0 and rec["expected_p50_ms"] > 0
+    f = rec["fixed_cost_us"]
+    assert abs(f["per_search_wall_us"] - f["hashing_at_kernel_rate_us"] - f["fixed_us"]) < 0.2
+    d = rec["decomposition_us"]
+    for k in ("gpu_idle_between_launches", "decided_to_result_in_client", "client_turnaround_to_next_submit",
+              "losers_stop_after_decide"):
+        assert k in d
+    chk = bench.device_check([4.3, 4.31, 4.29], 1000, 1000)
+    assert chk["ok"] and chk["slow_devices"] == []
+    bad = bench.device_check([4.3, 4.31, 3.5], 1000, 1000)
+    assert not bad["ok"] and bad["slow_devices"] == [2]
+    assert not bench.device_check([4.3, 4.3], 999, 1000)["ok"]  # counters that do not sum

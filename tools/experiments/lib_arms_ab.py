@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Interleaved A/B of libnanopow builds, each arm in its own process (round 5).
 
-Arms are NAME=PATH pairs (PATH = a libnanopow.so; "tree" = the in-tree library).  Per arm and round: 150
+Arms are NAME=PATH[@VAR=VAL[@VAR=VAL...]] (PATH = a libnanopow.so; "tree" = the in-tree library; the VAR=VAL pairs go
+into that arm's environment, e.g. tree@NANOPOW_WATCHER=0).  Per arm and round: 150
 send-difficulty searches one at a time (bench rate, kernel rate, in-kernel clock, SIMD cycles per 64-nonce hash)
 and 300 receive-difficulty searches (p50 / p90 wall time at the C ABI).  The order of the arms alternates by round.
 
@@ -45,8 +46,12 @@ print(json.dumps(out))
 """
 
 
-def arm(name, path, first):
+def arm(name, spec, first):
     env = dict(os.environ)
+    path, *extra = spec.split("@")
+    for kv in extra:
+        k, v = kv.split("=", 1)
+        env[k] = v
     if path != "tree":
         env["NANOPOW_LIB"] = os.path.abspath(path)
     code = f"ROOT = {ROOT!r}\nSEND = {SEND}\nRECEIVE = {RECEIVE}\nFIRST = {first}\n" + ARM
