@@ -404,6 +404,25 @@ int npow_init(int* n_devices) try {
     const char* vp = getenv("NANOPOW_VIRTUAL_PARTITION");
     if (!vp || strcmp(vp, "share") != 0) parts = n_logical / n;
   }
+  // Test hook (with NANOPOW_TEST_HOOKS=1): NANOPOW_TEST_EXTRA_QUEUES=n creates n more CU-masked streams on HIP device 0
+  // that nothing ever uses -- n more hardware queues of this process, idle -- to tell a queue count's effect on the
+  // CU-partition rehearsal from a partition size's
+  if (const char* q = test_hooks_enabled() ? getenv("NANOPOW_TEST_EXTRA_QUEUES") : nullptr) {
+    static std::vector<hipStream_t> extra;
+    static void* scratch = nullptr;
+    fprintf(stderr, "nanopow: TEST HOOKS ACTIVE: %s idle extra CU-masked streams\n", q);
+    HIPTRY(hipSetDevice(0));
+    if (!scratch) HIPTRY(hipMalloc(&scratch, 64));
+    for (int i = 0; i < atoi(q); ++i) {
+      uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      m[i % 8] = 1u << (i / 8);  // one CU each
+      hipStream_t st = nullptr;
+      HIPTRY(hipExtStreamCreateWithCUMask(&st, 8, m));
+      HIPTRY(hipMemsetAsync(scratch, 0, 64, st));  // one command, so that the stream holds its hardware queue
+      HIPTRY(hipStreamSynchronize(st));
+      extra.push_back(st);
+    }
+  }
   for (int i = 0; i < n_logical; ++i) {
     g_devs.push_back(std::make_unique<Device>());
     g_devs.back()->id = i;

@@ -196,7 +196,8 @@ struct alignas(64) PoolWin {
   uint64_t gen;
   uint64_t nonce;
   uint64_t value;
-  uint8_t pad[40];
+  uint64_t t;  // s_memrealtime (100 MHz) when the winning wave published (NANOPOW_TRACE_LATENCY timelines)
+  uint8_t pad[32];
 };
 // In-kernel clock of a search launch: the first wave of workgroups 0..7 (one per XCD) records
 // its s_memtime span (shader cycles) and s_memrealtime span (100 MHz) from its first to its
@@ -205,6 +206,7 @@ constexpr int kClkWaves = 8;
 struct PoolClk {
   uint64_t cycles, ref;
   uint32_t seq, pad;
+  uint64_t t0, t1;  // the recording wave's s_memrealtime at its first and last instruction (absolute, 100 MHz)
 };
 // Final nonce count of a closed entry (search kernels): the sum of the slot's done shards once
 // no workgroup is left on it and none can join, so a won or killed job finishes without waiting
@@ -213,7 +215,9 @@ struct alignas(64) PoolFin {
   uint64_t gen;    // released after total and late
   uint64_t total;  // the slot's done shards, summed (cumulative over its generations)
   uint64_t late;   // the slot's late words, summed (kLateWord; cumulative)
-  uint8_t pad[40];
+  uint64_t t_fin;    // s_memrealtime of the publication (NANOPOW_TRACE_LATENCY GPU timelines)
+  uint64_t t_relay;  // diagnostic builds (-DNPOW_DIAG_TIMES): s_memrealtime when a poll read the slot's kill word
+  uint8_t pad[24];
 };
 // An unbounded job adopted while a search launch runs joins that launch instead of ending it
 // (a yield): the host writes its entry at ring position p (dyn[p % kDynEntries]) and then releases

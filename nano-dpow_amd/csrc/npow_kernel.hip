@@ -341,6 +341,8 @@ __device__ __forceinline__ void clk_end_ls2(const PoolTable* tab, PoolMailbox* m
     PoolClk* r = &mb->clk[tab->ring & 3][blockIdx.x];
     __hip_atomic_store(&r->cycles, c_end - s_clk_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&r->ref, t_end - t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->t0, t_start, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&r->t1, t_end, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&r->seq, tab->seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -454,6 +456,7 @@ __device__ __forceinline__ void ls2_fin_wave(PoolDevState* st, PoolMailbox* mb, 
   if (lane == 0) {
     __hip_atomic_store(&mb->fin[slot].total, (uint64_t)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&mb->fin[slot].late, (uint64_t)t_late, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mb->fin[slot].t_fin, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&mb->fin[slot].gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
@@ -538,6 +541,7 @@ __device__ __forceinline__ void ls2_publish_win(PoolDevState* st, PoolMailbox* m
     PoolWin* pw = &mb->win[slot];
     __hip_atomic_store(&pw->nonce, wn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&pw->value, wv, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&pw->t, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     __hip_atomic_store(&pw->gen, gen, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     // the winner's own workgroup is on the entry: its leave publishes, after the win record
   }
@@ -623,6 +627,10 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
   }
   bool killed = false;
   if (__hip_atomic_load(&mb->kill[pe->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == pe->gen) {
+#ifdef NPOW_DIAG_TIMES
+    __hip_atomic_store(&mb->fin[pe->slot].t_relay, __builtin_amdgcn_s_memrealtime(), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
     ls2_kill(st, mb, pe->slot, pe->gen, tab->counted != 0);  // relay
     leave = killed = true;
   }
@@ -682,6 +690,10 @@ __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st
   }
   return kNoEntry;  // entries died under every attempt: the workgroup is finished
 }
+
+// Odd, so that it0 -> -it0 * kPollStride is a bijection modulo every power of two; its residues mod 2^10..2^13 step
+// by 0.43, 0.22, 0.11 and 0.80 of the range (the fractional part of the golden ratio in 32 bits).
+constexpr uint32_t kPollStride = 0x9E3779B9u;
 
 template <bool BOUNDED>
 __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab, PoolDevState* __restrict__ st,
@@ -776,7 +788,12 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
           ls2_publish_win(st, mb, ce->slot, ce->gen, wn, wval);
         }
       }
-      if (__builtin_expect(((it0 + w) & poll_mask) == 0, 0)) {
+      // which wave polls at iteration it0: the one with w = -it0 * kPollStride (mod poll_mask + 1) -- consecutive
+      // iterations' pollers spread over the grid (round 5).  With w = -it0 a launch's first ~100 polls all fell to its
+      // last-dispatched workgroups, the youngest and slowest on their SIMDs (VALU issue favours the oldest wave): on a
+      // grid of 1,024 waves (one 32-CU partition) a host kill then waited ~200 us for a poll instead of ~15
+      // (profiles/r05f_over_g8.err: relay p50 207 us after the win against 37 us on 64-CU partitions)
+      if (__builtin_expect(((it0 * kPollStride + w) & poll_mask) == 0, 0)) {
         if (lane == 0) s_flag[wv] = ls2_poll(tab, st, mb, e, &s_seen);  // the wave's own word
         lds_drain();
         const uint32_t p = __builtin_amdgcn_readfirstlane(

@@ -82,6 +82,14 @@ const double g_poll_us = [] {
   return e ? atof(e) : 50.0;
 }();
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
+// A slot whose job finished from its published final count is freed without reading its done counts back once the
+// launches that held it have completed, except every kVerifyEvery-th, which still checks the count against the
+// read-back (npow_device_stats.early_mismatches).  NANOPOW_READBACK=always reads every slot back (A/B runs).
+constexpr uint64_t kVerifyEvery = 16;
+const bool g_readback_always = [] {
+  const char* e = getenv("NANOPOW_READBACK");
+  return e && strcmp(e, "always") == 0;
+}();
 // The win watcher (watcher_run): on by default; NANOPOW_WATCHER=0 turns it off (A/B runs)
 const bool g_watcher_on = [] {
   const char* e = getenv("NANOPOW_WATCHER");
@@ -382,6 +390,7 @@ void watch_handle(Device& d, int s, uint64_t gen) {
   decide_locked(*j, NPOW_OK, n, v);
   j->t_decide = now_us();
   j->t_win_seen = t_seen;
+  j->gpu_t_win = __atomic_load_n(&pw.t, __ATOMIC_RELAXED);
   if (j->t_win == 0) j->t_win = t_seen;
   j->winner_k = k;
   stop_other_devices_locked(*j, (size_t)k);
@@ -447,6 +456,7 @@ struct Slot {
   bool requeue = false;    // invalid GPU result: hand the job back to this device after retiring
   bool no_more = false;    // bounded range fully issued
   bool readback = false;   // done-shard read-back queued (ev_done[slot] marks it)
+  bool no_readback = false;  // finished early and not sampled for verification: freed once inflight is empty
   bool fresh = false;      // adopted since the last launch was built
   bool new_job = false;    // adopted for the first time on this device (not a re-adoption)
   bool fin_seen = false;   // the kernel published this generation's final count (PoolMailbox::fin) ...
@@ -486,6 +496,7 @@ class Worker {
   uint64_t yields_ = 0;
   uint64_t ctl_ = 0;  // PoolMailbox::ctl (only this worker writes it): yields << 32 | dynamic entries
   uint64_t wake_seen_ = 0;  // Device::wake_seq as of this worker's last nap
+  uint64_t early_count_ = 0;  // slots finished early so far (every kVerifyEvery-th is still read back)
   int invalid_streak_ = 0;  // consecutive winners of this device that failed CPU re-validation
   int prev_stop_ring_ = -1;  // ring of the last retired launch (its stop event: the GPU idle before the next one),
                              // -1 when a sweep / values task used the device's events since
@@ -542,7 +553,7 @@ class Worker {
   uint64_t push_back_locked(Slot& sl, size_t from, bool skip_done = false);
   bool launch_completed(uint64_t seq) const;
   bool launch_started(uint64_t seq) const;
-  void account_clock(int ring, uint64_t seq);
+  void account_clock(int ring, uint64_t seq, uint64_t* t0 = nullptr, uint64_t* t1 = nullptr);
   int step();
   void nap();
 };
@@ -572,7 +583,7 @@ void Worker::adopt() {
     sl.job = j;
     sl.k = (size_t)k;
     sl.gen = ++g_gen;
-    sl.win_seen = sl.requeue = sl.no_more = sl.readback = sl.fin_seen = sl.early = false;
+    sl.win_seen = sl.requeue = sl.no_more = sl.readback = sl.fin_seen = sl.early = sl.no_readback = false;
     sl.stop_us = 0;
     sl.unread = 0;
     sl.fresh = true;
@@ -705,6 +716,7 @@ void Worker::handle_win(int s) {
       decide_locked(j, NPOW_OK, n, v);
       j.t_decide = now_us();
       j.t_win_seen = t_seen;
+      j.gpu_t_win = __atomic_load_n(&pw.t, __ATOMIC_RELAXED);
       j.winner_k = (int)sl.k;
       stop_other_devices_locked(j, sl.k);
     }
@@ -785,11 +797,16 @@ bool Worker::launch_completed(uint64_t seq) const {
 }
 
 // The launch's in-kernel clock records (PoolClk, one per XCD) into the device statistics.
-void Worker::account_clock(int ring, uint64_t seq) {
+void Worker::account_clock(int ring, uint64_t seq, uint64_t* t0, uint64_t* t1) {
   double cyc = 0, ref = 0;
   for (int x = 0; x < kClkWaves; ++x) {
     const PoolClk& c = d_.pmb->clk[ring][x];
     if (__atomic_load_n(&c.seq, __ATOMIC_ACQUIRE) != (uint32_t)seq) continue;
+    if (t0) {  // the launch's span on the GPU's realtime clock: the earliest start, the latest end of the records
+      const uint64_t a = __atomic_load_n(&c.t0, __ATOMIC_RELAXED), b = __atomic_load_n(&c.t1, __ATOMIC_RELAXED);
+      if (*t0 == 0 || a < *t0) *t0 = a;
+      if (b > *t1) *t1 = b;
+    }
     const double cy = (double)__atomic_load_n(&c.cycles, __ATOMIC_RELAXED);
     const double rf = (double)__atomic_load_n(&c.ref, __ATOMIC_RELAXED);
     // a record from a wave that ran for a few ticks only (a launch that found its job already over) is
@@ -820,6 +837,13 @@ void Worker::early_finish(int s) {
   const uint64_t late = __atomic_load_n(&d_.pmb->fin[s].late, __ATOMIC_RELAXED);
   std::lock_guard<std::mutex> g(g_pool.mu);
   Job& j = *sl.job;
+  if (g_trace_lat && j.gpu_t_win) {  // GPU timeline (one GPU's clock: CU partitions), from the deciding win
+    const double tw = (double)j.gpu_t_win, tr = (double)__atomic_load_n(&d_.pmb->fin[s].t_relay, __ATOMIC_RELAXED);
+    fprintf(stderr, "nanopow-fin dev %d ticket %llu: relay %+.1f fin %+.1f seen %+.1f us (host) from the win%s\n", d_.id,
+            (unsigned long long)j.ticket, (tr - tw) / 100.0,
+            ((double)__atomic_load_n(&d_.pmb->fin[s].t_fin, __ATOMIC_RELAXED) - tw) / 100.0,
+            j.t_win_seen > 0 ? now_us() - j.t_win_seen : -1.0, (int)sl.k == j.winner_k ? " (winner)" : "");
+  }
   if (d_.dead || sl.requeue || !j.decided.load()) return;
   sl.early = true;
   const uint64_t delta = total - sl.baseline;
@@ -995,13 +1019,28 @@ int Worker::launch() {
 }
 
 // Slots that just left the tables: read their done shards back in stream order, behind every
-// launch that still holds them (later launches do not), and note when that copy lands.
+// launch that still holds them (later launches do not), and note when that copy lands.  Round 5: a won or killed
+// slot's kernels publish its final count (every launch, one-entry ones included), so the read-back -- a copy on the
+// stream between the dying launch and the next search's launch, ~GPU idle on every device each search -- waits for
+// that record: a slot finished from it is freed without a read-back once its launches have completed (every
+// kVerifyEvery-th still reads back and checks), and the read-back runs only when no record came (the launches ended
+// first: a kill that no poll relayed before the budget ran out; a bounded range exhausted; an invalid win).
 int Worker::queue_readbacks() {
   constexpr size_t row = kPoolDoneShards * 8;
   DEVCHECK(d_, "pool read-back");
   for (int s = 0; s < kMaxSlots; ++s) {
     Slot& sl = slots_[s];
-    if (sl.state != SlotState::kDraining || sl.readback) continue;
+    if (sl.state != SlotState::kDraining || sl.readback || sl.no_readback) continue;
+    if (!g_readback_always && !d_.dead) {
+      if (sl.early) {
+        if (++early_count_ % kVerifyEvery != 0) {
+          sl.no_readback = true;
+          continue;
+        }
+      } else if (!sl.fin_seen && sl.stop_us > 0 && !sl.requeue && !sl.inflight.empty()) {
+        continue;  // won or killed: its final count is on the way (or its launches end without one)
+      }
+    }
     HIPTRY(hipMemcpyAsync(d_.h_done + (size_t)s * row, &d_.pst->done[s][0], row * sizeof(unsigned long long),
                           hipMemcpyDeviceToHost, d_.stream));
     HIPTRY(hipEventRecord(d_.ev_done[s], d_.stream));
@@ -1029,7 +1068,16 @@ int Worker::retire() {
       }
     }
     prev_stop_ring_ = q_.front().ring;
-    account_clock(q_.front().ring, q_.front().seq);
+    uint64_t g0 = 0, g1 = 0;
+    account_clock(q_.front().ring, q_.front().seq, &g0, &g1);
+    if (g_trace_lat && g0)  // GPU timeline of a decided job's launch on this device, from the deciding win (the same
+                            // clock only for devices on one GPU: CU partitions)
+      for (const Slot& sl : slots_)
+        if (sl.state != SlotState::kFree && sl.job && sl.job->gpu_t_win && !sl.inflight.empty() &&
+            sl.inflight.front().seq <= q_.front().seq)
+          fprintf(stderr, "nanopow-gpu dev %d ticket %llu launch %llu: start %+.1f end %+.1f us from the win\n", d_.id,
+                  (unsigned long long)sl.job->ticket, (unsigned long long)q_.front().seq,
+                  ((double)g0 - (double)sl.job->gpu_t_win) / 100.0, ((double)g1 - (double)sl.job->gpu_t_win) / 100.0);
     // The launch's ranges are complete, except those of a generation that won in it (or in an
     // earlier launch still unseen): handle such wins first, they hand back what did not finish.
     const uint64_t seq = q_.front().seq;
@@ -1063,6 +1111,14 @@ int Worker::retire() {
   constexpr size_t row = kPoolDoneShards * 8;
   for (int s = 0; s < kMaxSlots; ++s) {
     Slot& sl = slots_[s];
+    if (sl.state == SlotState::kDraining && sl.no_readback && sl.inflight.empty()) {
+      // finished from its published final count and every launch that held it has completed: nothing can still add
+      // to its done counts, so the next job of this slot starts from the published total (sl.baseline)
+      watch_disarm(d_, s);
+      sl.job.reset();
+      sl.state = SlotState::kFree;
+      continue;
+    }
     if (sl.state != SlotState::kDraining || !sl.readback) continue;
     const hipError_t e = hipEventQuery(d_.ev_done[s]);
     if (e == hipErrorNotReady) continue;

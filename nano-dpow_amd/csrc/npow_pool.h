@@ -66,6 +66,7 @@ struct Job {
   // NANOPOW_TRACE_LATENCY, which prints the timeline in pool_wait).  t_win: the first win record read; t_win_seen:
   // the deciding one (CPU re-validation then decides at t_decide)
   double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0, t_decide = 0, t_win_seen = 0;
+  uint64_t gpu_t_win = 0;  // the deciding win's s_memrealtime (PoolWin::t; NANOPOW_TRACE_LATENCY GPU timelines)
 };
 using JobP = std::shared_ptr<Job>;
 

@@ -29,23 +29,26 @@ def pct(xs, p):
     return xs[min(len(xs) - 1, max(0, int(round(p / 100.0 * (len(xs) - 1)))))]
 
 
-def main(n_search, which):
+def main(n_search, which, mask=0):
+    """mask != 0: split every search over those devices only (the others idle): e.g. 4 of 8 CU partitions, to tell
+    the engine's stop path from the hardware queues' scheduling of 5+ concurrently busy CU-masked queues."""
     eng = _lib.Engine()
-    G = eng.n_devices
+    G = eng.n_devices if not mask else bin(mask).count("1")
     thr = THRESHOLDS[which]
     rng = random.Random(11)
     spans, over, done, ttw, winners, late_l, late_w, res_ms = [], [], [], [], [], [], [], []
     for i in range(n_search):
         root = bytes(rng.getrandbits(8) for _ in range(32))
         t0 = time.perf_counter()
-        t = eng.submit(root, thr, start=rng.getrandbits(64), device_mask=0)
+        t = eng.submit(root, thr, start=rng.getrandbits(64), device_mask=mask)
         r = t.wait_result(120)  # the outcome at the decision (what a client is answered with)
         res_ms.append((time.perf_counter() - t0) * 1e3)
         info = t.wait_info(120)
         assert r.status == info.status and r.nonce == info.nonce
         assert info is not None and info.status == _lib.NPOW_OK, info
         assert oracle.work_value_hashlib(root, info.nonce) == info.value >= thr
-        assert info.n_devices == G and 0 <= info.winner_device < G
+        assert info.n_devices == G and 0 <= info.winner_device < eng.n_devices
+        assert not mask or (mask >> info.winner_device) & 1
         spans.append(info.stop_after_decide_us)
         over.append(info.overshoot_nonces)
         late_l.append(info.late_nonces_losers)
@@ -53,7 +56,7 @@ def main(n_search, which):
         done.append(info.nonces_done)
         ttw.append(info.finish_us)
         winners.append(info.winner_device)
-    st = [eng.stats(d) for d in range(G)]
+    st = [eng.stats(d) for d in range(eng.n_devices) if not mask or (mask >> d) & 1]
     kills = sum(x.kills_relayed for x in st)
     # the losers' late hashes are deterministic: in each losing device's one-entry launch every workgroup but the
     # one whose poll read the kill word sees the relayed dead word before a hash and leaves after it -- one hash of
@@ -82,4 +85,4 @@ def main(n_search, which):
 
 
 if __name__ == "__main__":
-    main(int(sys.argv[1]), sys.argv[2])
+    main(int(sys.argv[1]), sys.argv[2], int(sys.argv[3], 0) if len(sys.argv) > 3 else 0)
