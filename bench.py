@@ -1369,6 +1369,16 @@ def node_regime(eng, n_dev: int, m: int, thr: int = REGIME, http_m: int = 0):
     one keep-alive connection (the HTTP hop)."""
     import queue
     mask = (1 << n_dev) - 1
+    # The devices' full rate, for reference (round 5): one search that cannot end (threshold 2^64 - 1) over every
+    # device, cancelled after 0.4 s -- nonces / wall.  With lingering launches (a launch waits in the GPU for the next
+    # search) the kernels' event time includes the waits between searches, so the kernel rate below is no longer
+    # the rate the devices hash at; this is.
+    t_ref = time.perf_counter()
+    tk_ref = eng.submit(bench_root(6_950_000), (1 << 64) - 1, start=0, device_mask=mask)
+    time.sleep(0.4)
+    tk_ref.cancel()
+    ref_info = tk_ref.wait_info()
+    ref_rate = ref_info.nonces_done / (time.perf_counter() - t_ref)
     for w in range(5):
         search_to_result(eng, bench_root(6_900_000 + w), thr, bench_start(w), mask)
     for d in range(n_dev):
@@ -1424,10 +1434,17 @@ def node_regime(eng, n_dev: int, m: int, thr: int = REGIME, http_m: int = 0):
         "kernel_gnps": round(kern_rate / 1e9, 4),
         "node_gnps": round(node_gnps, 4),
         "node_over_kernel": round(node_gnps * 1e9 / kern_rate, 4),
+        "reference_gnps": round(ref_rate / 1e9, 4),
+        "node_over_reference": round(node_gnps * 1e9 / ref_rate, 4),
+        "p50_minus_expected_at_reference_ms": round(pct(res, 50) * 1e3 - ln2 * E / ref_rate * 1e3, 4),
+        "reference_what": "every device on one search that cannot end, cancelled after 0.4 s: its nonces / wall -- "
+                          "the devices' full rate; with lingering launches the kernel rate above (HIP events) "
+                          "includes the launches' waits for the next search",
         "expected_p50_ms": round(ln2 * E / kern_rate * 1e3, 4),
         "expected_mean_ms": round(E / kern_rate * 1e3, 4),
         "p50_minus_expected_ms": round(pct(res, 50) * 1e3 - ln2 * E / kern_rate * 1e3, 4),
         "nonces_per_search_over_E": round(statistics.mean(done) / E, 4),
+        "fixed_cost_at_reference_us": round(per_search_us - statistics.mean(done) / ref_rate * 1e6, 1),
         "fixed_cost_us": {
             "per_search_wall_us": round(per_search_us, 1),
             "hashing_at_kernel_rate_us": round(hashing_us, 1),
@@ -1455,6 +1472,8 @@ def node_regime(eng, n_dev: int, m: int, thr: int = REGIME, http_m: int = 0):
                     "once a launch is 0.4 ms old), decided after CPU re-validation, the result in the client's "
                     "thread (Python), the client's turnaround to the next submit, the losing devices' stop as the "
                     "host saw it, the ticket collected (every device stopped)"},
+        "launches_per_search_per_device": round(sum(k.launches for k in ks) / (m * n_dev), 3),
+        "dyn_entries_per_search_per_device": round(sum(k.dyn_entries for k in ks) / (m * n_dev), 3),
         "late_nonces_losers": _mean_p([x.late_nonces_losers for x in infos]),
         "per_device_kernel_gnps": [round(k.nonces / (k.kernel_ms * 1e-3) / 1e9, 4) if k.kernel_ms > 0 else None
                                    for k in ks],

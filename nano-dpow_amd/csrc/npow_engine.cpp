@@ -426,6 +426,8 @@ int npow_init(int* n_devices) try {
   for (int i = 0; i < n_logical; ++i) {
     g_devs.push_back(std::make_unique<Device>());
     g_devs.back()->id = i;
+    // several logical devices time-sharing one GPU's CUs: a lingering launch would hold them from the others
+    g_devs.back()->time_shared = n_logical > n && parts == 1;
     if (int rc = init_device(*g_devs.back(), n, parts)) {
       // leave nothing behind: a retried npow_init starts from an empty device list
       const std::string msg = last_error();

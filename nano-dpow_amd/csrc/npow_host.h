@@ -38,6 +38,7 @@ struct Device {
   int cpu_threads = 0;  // > 0: not a GPU but the pool's CPU workers (npow_cpu.cpp, --cpu-threads); no HIP state
   int hip_id = 0;   // HIP device (== id unless NANOPOW_VIRTUAL_DEVICES is set)
   int cus = 0;       // CUs the device's kernels run on (its partition's, see cu_first)
+  bool time_shared = false;  // one of several logical devices time-sharing a GPU (NANOPOW_VIRTUAL_PARTITION=share)
   int cu_first = -1; // -1: the whole GPU; else the first CU of this logical device's partition (a CU-masked
                      // stream over [cu_first, cu_first + cus) of HIP device hip_id; npow_engine.cpp init_device)
   hipStream_t stream = nullptr;
@@ -63,6 +64,7 @@ struct Device {
   uint64_t launches = 0, nonces = 0, invalid = 0;
   uint64_t early = 0, early_mismatch = 0;  // jobs finished from a published final count (npow_pool.cpp)
   uint64_t yields = 0, dyn = 0;            // launches yielded / jobs that joined a running launch
+  uint64_t linger_ends = 0;                // lingering launches ended early (Worker::end_linger)
   uint64_t kills_relayed = 0;              // losing jobs stopped by another device's decision (npow_pool.cpp)
   uint64_t late = 0;                       // device-side overshoot: nonces hashed after the job was known over
   uint64_t watcher_decisions = 0;          // jobs the win watcher decided from this device's win records

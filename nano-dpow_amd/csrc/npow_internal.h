@@ -131,7 +131,10 @@ struct PoolTable {
                           // launch with one entry ends with it, and counting only slows its end.
   uint32_t kill_base;     // the low half of PoolMailbox::kills when the table was built: a polling wave that
                           // reads another value relays the kill words of every entry, not only its own
-  uint32_t pad[5];
+  uint32_t linger;        // search kernels (counted launches, round 5): a workgroup that finds no live entry waits
+                          // in the launch for the host's next dynamic entry (ls2_linger) until the time budget
+                          // ends or a yield, instead of leaving -- the next search needs no launch
+  uint32_t pad[4];
   PoolEntry e[kMaxSlots];
 };
 inline size_t pool_table_bytes(uint32_t n) { return offsetof(PoolTable, e) + (size_t)n * sizeof(PoolEntry); }
@@ -188,6 +191,10 @@ struct PoolDevState {
   // holding other entries must not skip the scan because another launch relayed up to the same count.
   alignas(64) unsigned long long kills_done[kPoolRing][8];
   PoolExit exits[kPoolRing];
+  // The latest PoolMailbox::ctl a lingering workgroup read from the pinned word (ls2_linger), for the other
+  // lingering workgroups to read from device memory: one uncached host read per 64 lingering workgroups' looks
+  // instead of one each.  Monotonic like ctl; a value older than a launch's table reads as no news (ls2_mirror_ok).
+  alignas(64) unsigned long long ctl_mirror[8];
 };
 
 // Pinned host-coherent mailbox of the pool: one win record per slot (the winner stores

@@ -575,6 +575,23 @@ __device__ __forceinline__ uint32_t ls2_dyn_count(const PoolTable* tab, uint64_t
   const uint32_t d = (uint32_t)ctl - tab->dyn_base;
   return d < (uint32_t)kDynEntries ? d : (uint32_t)kDynEntries;
 }
+// The same for a value that may predate the launch's table (PoolDevState::ctl_mirror): none then.
+__device__ __forceinline__ uint32_t ls2_dyn_count_since(const PoolTable* tab, uint64_t ctl) {
+  const int32_t d = (int32_t)((uint32_t)ctl - tab->dyn_base);
+  return d <= 0 ? 0u : (d < kDynEntries ? (uint32_t)d : (uint32_t)kDynEntries);
+}
+
+// The launch's entries this workgroup knows to be over (bit k: entry k -- dead, or bounded, which no workgroup moves
+// to): an entry's header (slot, generation) is read from the table or from the pinned dynamic ring, uncached over PCIe
+// for every lane that looks at it, so a lingering launch, whose ring fills with the serial client's finished
+// searches, would otherwise re-read every one of them at each pick and at each balancing poll (round 5).  An entry
+// once dead stays dead (its slot's dead word only grows), so the mask is exact.  Wave 0 picks; any wave's poll may
+// add bits (an LDS atomic or).
+__shared__ unsigned long long s_over;
+__device__ __forceinline__ void ls2_mark_over(unsigned long long bits) {
+  if (bits) __hip_atomic_fetch_or(&s_over, bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // Occupancy for balancing: this XCD shard's workgroups on the entry (workgroups are dealt to the XCDs
 // round-robin, so balancing each shard balances the whole).
 __device__ __forceinline__ unsigned long long ls2_wgs(PoolDevState* st, uint32_t slot) {
@@ -592,9 +609,11 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
   const uint64_t ctl = ls2_ctl(mb);
   // (a one-entry launch -- uncounted -- holds only the entry whose kill word this poll reads below: no read of
   // the counter there, whose uncached read at every poll was 0.76 MB per 10-ms launch of PMC traffic)
-  const uint32_t kills = tab->counted ? (uint32_t)__hip_atomic_load(&mb->kills, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                                      : tab->kill_base;
+  // (nor in a launch of one entry so far: a lingering launch is counted from its first entry on)
   const uint32_t nd = ls2_dyn_count(tab, ctl);
+  const uint32_t kills = tab->counted && tab->n + nd > 1
+                             ? (uint32_t)__hip_atomic_load(&mb->kills, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                             : tab->kill_base;
   ls2_fresh(nd, seen);
   bool leave = false;
   // A job of this launch was killed since it was built, and no wave has relayed that kill yet: relay every such
@@ -610,7 +629,9 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
   const unsigned long long key = ((unsigned long long)tab->seq << 32) | kills;
   if (kills != tab->kill_base && __hip_atomic_load(kd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != key) {
     __atomic_signal_fence(__ATOMIC_SEQ_CST);
+    const unsigned long long over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
+      if ((over >> k) & 1) continue;
       ConstEntry* q = ls2_entry(tab, mb, k);
       if (load_dead(st, q->slot) < q->gen &&
           __hip_atomic_load(&mb->kill[q->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q->gen)
@@ -636,44 +657,44 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
   }
   if (!leave && !pe->bounded && nd > 0) {
     const unsigned long long mine = ls2_wgs(st, pe->slot);
+    const unsigned long long over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    unsigned long long found = 0;
     for (uint32_t k = tab->n; k < tab->n + nd && !leave; ++k) {
-      if (k == e) continue;
+      if (k == e || ((over >> k) & 1)) continue;
       ConstEntry* q = ls2_entry(tab, mb, k);
-      leave = load_dead(st, q->slot) < q->gen && ls2_wgs(st, q->slot) + 2 <= mine;
+      if (q->bounded || load_dead(st, q->slot) >= q->gen) {
+        found |= 1ull << k;
+        continue;
+      }
+      leave = ls2_wgs(st, q->slot) + 2 <= mine;
     }
+    ls2_mark_over(found);
   }
   return (leave ? 1u : 0u) | (killed ? 2u : 0u);
 }
 
-// Wave 0 (every lane): the entry the workgroup works on next, joined; kNoEntry if none can be.  At
-// the launch's start (first) its own entry e, bounded or not, if it can be joined; otherwise the
-// live unbounded entry with the fewest workgroups, ties broken by a hash of the workgroup index so
-// that the workgroups leaving one entry spread over the others.  Each lane looks at one entry.
-__device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
-                                          bool first, uint32_t* seen) {
-  // the lane from mbcnt, not threadIdx: a callee that reads the work-item id makes every wave keep
-  // (and spill) the register the ABI passes it in
-  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)), g = blockIdx.x;
-  if (first) {
-    uint32_t ok = 0;
-    if (lane == 0) {
-      ConstEntry* pe = ls2_entry(tab, mb, e);
-      ok = ls2_join(st, mb, pe->slot, pe->gen, tab->counted != 0) ? 1u : 0u;  // (the join checks dead itself)
-    }
-    if (__builtin_amdgcn_readfirstlane(ok)) return e;
-  }
-  const uint32_t nd = ls2_dyn_count(tab, ls2_ctl(mb));
+// Wave 0 (every lane): of the launch's first nd dynamic entries and its table's, the live unbounded entry other than e
+// with the fewest workgroups, joined, ties broken by a hash of the workgroup index so that the workgroups leaving one
+// entry spread over the others; kNoEntry if none can be.  Each lane looks at one entry.
+__device__ __forceinline__ uint32_t ls2_choose(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
+                                               uint32_t nd, uint32_t* seen, uint32_t lane, uint32_t g) {
   const uint32_t N = tab->n + nd;  // <= kMaxSlots = 64: one lane each
   ls2_fresh(nd, seen);
   for (int attempt = 0; attempt < 4; ++attempt) {
     unsigned long long key = ~0ull;
-    if (lane < N && lane != e) {
+    bool over = false;
+    const unsigned long long known = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (lane < N && lane != e && !((known >> lane) & 1)) {
       ConstEntry* q = ls2_entry(tab, mb, lane);
       if (!q->bounded && load_dead(st, q->slot) < q->gen) {
         const uint32_t tie = ((lane + 1u) * 0x9e3779b1u) ^ (g * 0x85ebca6bu);
         key = (ls2_wgs(st, q->slot) << 32) | (tie & ~63u) | lane;
+      } else {
+        over = true;
       }
     }
+    const unsigned long long now_over = __ballot(over);
+    if (lane == 0) ls2_mark_over(now_over);
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) {
       const unsigned long long o = __shfl_xor(key, m);
@@ -688,7 +709,75 @@ __device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st
     }
     if (__builtin_amdgcn_readfirstlane(ok)) return pick;
   }
-  return kNoEntry;  // entries died under every attempt: the workgroup is finished
+  return kNoEntry;  // entries died under every attempt
+}
+
+// Wave 0 (every lane) of a workgroup of a lingering launch (PoolTable::linger, round 5) that found no live entry to
+// move to: wait in the launch for the host's next dynamic entry instead of leaving it, so that a serial client's next
+// search starts without a launch (its dispatch, the stream's events, the host's launch call and the cold start: the
+// GPU's gap between two searches was ~35 us on one device and ~110 us on each of 8 CU partitions,
+// tools/experiments/launch_spans.py).  Returns the entry joined, or kNoEntry once the host raised a yield (it ends a
+// lingering launch that a new launch must follow: a bounded job, a sweep, shutdown, the launch's time budget over --
+// Worker::end_linger) or after a budget's worth of lingering (a host that stopped looking).
+// The pinned word is read by ~2 lingering workgroups per look period grid-wide (phase (k + g) mod P, P ~ G / 2), each
+// of which raises PoolDevState::ctl_mirror to it; the others look at the mirror in device memory.  Between looks the
+// wave sleeps ~1.8 us (s_sleep 64: 64 x 64 clocks); the other waves of the workgroup wait at the barrier after it.
+__device__ __forceinline__ uint32_t ls2_linger(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t* seen,
+                                            uint32_t looked) {
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+  const uint32_t g = blockIdx.x, G = gridDim.x;
+  uint32_t P = 1;
+  while (P * 2 < G) P <<= 1;
+  unsigned long long* const mirror = &st->ctl_mirror[0];
+  const uint32_t base_hi = (uint32_t)(tab->yield_base >> 32);
+  const uint32_t t_enter = (uint32_t)__builtin_amdgcn_s_memrealtime();
+  for (uint32_t k = 0;; ++k) {
+    if ((uint32_t)__builtin_amdgcn_s_memrealtime() - t_enter >= tab->budget) return kNoEntry;
+    uint64_t ctl;
+    if (((k + g) & (P - 1)) == 0) {
+      ctl = ls2_ctl(mb);
+      __hip_atomic_fetch_max(mirror, (unsigned long long)ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      ctl = __hip_atomic_load(mirror, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint32_t hi = (uint32_t)(ctl >> 32);
+    if ((int32_t)(hi - base_hi) > 0) return kNoEntry;  // a yield since the table was built
+    if (hi == base_hi) {                               // (an older mirror value: no news)
+      const uint32_t nd = ls2_dyn_count_since(tab, ctl);
+      if (nd > looked) {
+        const uint32_t p = ls2_choose(tab, st, mb, kNoEntry, nd, seen, lane, g);
+        if (p != kNoEntry) return p;
+        looked = nd;  // (joined by others and over already, or cancelled)
+      }
+    }
+    __builtin_amdgcn_s_sleep(64);
+  }
+}
+
+// Wave 0 (every lane): the entry the workgroup works on next, joined; kNoEntry if none can be.  At
+// the launch's start (first) its own entry e, bounded or not, if it can be joined; otherwise another
+// live unbounded entry (ls2_choose).
+__device__ __noinline__ uint32_t ls2_pick(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
+                                          bool first, uint32_t* seen) {
+  // the lane from mbcnt, not threadIdx: a callee that reads the work-item id makes every wave keep
+  // (and spill) the register the ABI passes it in
+  const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)), g = blockIdx.x;
+  if (first) {
+    uint32_t ok = 0;
+    if (lane == 0) {
+      ConstEntry* pe = ls2_entry(tab, mb, e);
+      ok = ls2_join(st, mb, pe->slot, pe->gen, tab->counted != 0) ? 1u : 0u;  // (the join checks dead itself)
+    }
+    if (__builtin_amdgcn_readfirstlane(ok)) return e;
+  }
+  // the dynamic entries published so far: the pinned word -- or in a lingering launch leaving an entry the mirror
+  // (all its workgroups leave a won entry at once: ~G uncached reads of the pinned word together otherwise), which
+  // may be older: ls2_linger then learns of the newer ones
+  const bool lg = !first && tab->linger;
+  const uint32_t nd = lg ? ls2_dyn_count_since(tab, __hip_atomic_load(&st->ctl_mirror[0], __ATOMIC_RELAXED,
+                                                                       __HIP_MEMORY_SCOPE_AGENT))
+                         : ls2_dyn_count(tab, ls2_ctl(mb));
+  return ls2_choose(tab, st, mb, e, nd, seen, lane, g);
 }
 
 // Odd, so that it0 -> -it0 * kPollStride is a bijection modulo every power of two; its residues mod 2^10..2^13 step
@@ -712,7 +801,10 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
   if (threadIdx.x < 3) s_stop[threadIdx.x] = ~0u;
   const bool counted = tab->counted != 0;
   if (wv == 0) {
-    if (lane == 0) s_seen = 0;
+    if (lane == 0) {
+      s_seen = 0;
+      s_over = 0;
+    }
     // its own entry first.  An uncounted (one-entry) launch only checks that it is live: it may follow
     // a counted launch that held the same entry and has published its final count, after which no
     // nonce may be hashed for it (tests/test_gpu_configs.py caught one launch doing so).
@@ -732,12 +824,21 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
 
   uint32_t e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
   uint32_t seg = 0, it = 0;
+  uint32_t pc = w;  // the poll phase, (iterations on the entry) * kPollStride + w: carried through the loop (the
+                    // invariant w, beside it, was spilled and reloaded with a v_readlane every iteration once
+                    // ls2_linger was called)
   bool end = false;
+  for (;;) {  // a lingering launch: rounds of entries, each after the workgroup waited for the next one (ls2_linger)
   for (;;) {
     if (e == kNoEntry) break;
     const PoolEntry* pe = (const PoolEntry*)ls2_entry(tab, mb, e);
     PoolCursor c;
     pool_load_ls(pe, c, g, wv, G, n, e, iters);
+    // the poll phase restarts with each entry: the workgroups that join one together (a launch's start, a lingering
+    // launch's next search) then hash it in step, so exactly one wave in poll_mask + 1 polls per iteration; carried
+    // on from the launch's start instead, the phases of workgroups that had lingered apart drifted and the polls
+    // came at random (a tail on the losers' stop span over CU partitions)
+    pc = w;
     const uint32_t sw = seg % 3;
     const uint32_t poll_mask = tab->poll_mask, budget = tab->budget;
     unsigned long long* const dead_p = &st->slot[c.slot].dead;
@@ -758,10 +859,12 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
         end = (v & 3u) == 0;
         break;
       }
-      const uint32_t it0 = it;  // the poll phase
+      const uint32_t it0 = it;
+      const uint32_t pc0 = pc;  // the poll phase of iteration it0
       const uint64_t thr = c.threshold, gen = c.gen;
       const uint64_t value = npow_asm_work_value_lockstep_ld(nonce, c.up);
       ++it;
+      pc += kPollStride;
       bool hit = value >= thr;
       if constexpr (BOUNDED) {
         const uint32_t in_lanes = b < c.last_b ? 64u : (b == c.last_b ? c.tail : 0u);
@@ -793,7 +896,7 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
       // last-dispatched workgroups, the youngest and slowest on their SIMDs (VALU issue favours the oldest wave): on a
       // grid of 1,024 waves (one 32-CU partition) a host kill then waited ~200 us for a poll instead of ~15
       // (profiles/r05f_over_g8.err: relay p50 207 us after the win against 37 us on 64-CU partitions)
-      if (__builtin_expect(((it0 * kPollStride + w) & poll_mask) == 0, 0)) {
+      if (__builtin_expect((pc0 & poll_mask) == 0, 0)) {
         if (lane == 0) s_flag[wv] = ls2_poll(tab, st, mb, e, &s_seen);  // the wave's own word
         lds_drain();
         const uint32_t p = __builtin_amdgcn_readfirstlane(
@@ -850,6 +953,20 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     __syncthreads();
     e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
     ++seg;
+  }
+  // no entry to move to (the loop ended on kNoEntry, not on the budget or the iteration cap): a lingering launch's
+  // workgroup waits for the host's next one.  (Called here, after the entry loop, and not from ls2_pick: a callee
+  // there clobbering more registers made the search loop reload 4 more spilled SGPRs every iteration.)
+  if constexpr (BOUNDED) break;  // (the host sets linger only for launches of unbounded entries)
+  if (e != kNoEntry || !tab->linger) break;
+  __syncthreads();  // every wave has read s_next before wave 0 writes it again
+  if (wv == 0) {
+    const uint32_t next = ls2_linger(tab, st, mb, &s_seen, 0);
+    if (lane == 0) s_next = next;
+  }
+  __syncthreads();
+  e = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_next, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+  if (e == kNoEntry) break;
   }
   if (!counted && wv == 0) ls2_exit(tab, st, mb, G, g);  // the one-entry launch's end record (round 5)
   clk_end_ls2(tab, mb, t_start, wv);

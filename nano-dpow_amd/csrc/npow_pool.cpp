@@ -82,6 +82,19 @@ const double g_poll_us = [] {
   return e ? atof(e) : 50.0;
 }();
 const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
+// Lingering launches (round 5, PoolTable::linger): an unbounded launch's workgroups wait in it for the next dynamic
+// entry once its entries are over, so a serial client's next search joins the running launch instead of needing one.
+// The worker ends a launch that has lingered g_linger_us with nothing to do (end_linger): its sleeping waves hold the
+// CUs, and a serial client's next search comes within ~0.1 ms.  NANOPOW_LINGER=0 turns it off (A/B runs),
+// NANOPOW_LINGER_US sets the wait.  Off for logical devices that time-share a GPU (Device::time_shared).
+const bool g_linger = [] {
+  const char* e = getenv("NANOPOW_LINGER");
+  return !(e && e[0] == '0');
+}();
+const double g_linger_us = [] {
+  const char* e = getenv("NANOPOW_LINGER_US");
+  return e ? atof(e) : 1000.0;
+}();
 // A slot whose job finished from its published final count is freed without reading its done counts back once the
 // launches that held it have completed, except every kVerifyEvery-th, which still checks the count against the
 // read-back (npow_device_stats.early_mismatches).  NANOPOW_READBACK=always reads every slot back (A/B runs).
@@ -147,6 +160,14 @@ const Faults& faults() {
 #define NPOW_DBG(...)                     \
   do {                                    \
     if (g_debug) fprintf(stderr, __VA_ARGS__); \
+  } while (0)
+// the same with the steady clock's time first (ms; Python's time.monotonic() * 1e3 reads the same clock)
+#define NPOW_DBGT(...)                                        \
+  do {                                                        \
+    if (g_debug) {                                            \
+      fprintf(stderr, "[%.3f] ", now_us() * 1e-3);            \
+      fprintf(stderr, __VA_ARGS__);                           \
+    }                                                         \
   } while (0)
 
 }  // namespace
@@ -477,6 +498,7 @@ struct PoolInflight {
   uint64_t dyn_base;    // PoolTable::dyn_base of the launch
   uint64_t yield_base;  // PoolTable::yield_base of the launch
   bool counted;         // PoolTable::counted: early finish and dynamic entries are on in it
+  bool linger;          // PoolTable::linger: its workgroups wait for dynamic entries until its budget or a yield
 };
 
 class Worker {
@@ -497,9 +519,11 @@ class Worker {
   uint64_t ctl_ = 0;  // PoolMailbox::ctl (only this worker writes it): yields << 32 | dynamic entries
   uint64_t wake_seen_ = 0;  // Device::wake_seq as of this worker's last nap
   uint64_t early_count_ = 0;  // slots finished early so far (every kVerifyEvery-th is still read back)
+  double idle_since_ = 0;     // launches in flight but no live slot since (end_linger after g_linger_us), 0 = busy
   int invalid_streak_ = 0;  // consecutive winners of this device that failed CPU re-validation
   int prev_stop_ring_ = -1;  // ring of the last retired launch (its stop event: the GPU idle before the next one),
                              // -1 when a sweep / values task used the device's events since
+  uint64_t prev_g1_ = 0;     // NANOPOW_TRACE_LATENCY: the previous launch's end on the GPU clock
   struct StepProf {
     uint64_t n = 0, slow = 0;
     double total = 0, max = 0;
@@ -536,6 +560,12 @@ class Worker {
   void adopt();
   void yield_if_long();
   bool dyn_add(int s);
+  bool live_slot() const {  // a slot some launch in flight (or a dynamic entry) is hashing
+    for (const Slot& sl : slots_)
+      if (sl.state == SlotState::kActive && !sl.fresh) return true;
+    return false;
+  }
+  void end_linger();
   void handle_win(int s);
   bool win_published(int s) const;
   void early_finish(int s);
@@ -600,19 +630,24 @@ void Worker::adopt() {
   // Unbounded jobs join the running launch as dynamic entries (no yield: the launch goes
   // on and workgroups move to them); a new job that cannot ends the long launch instead.
   bool waiting_new = false;
+  const uint64_t ctl0 = ctl_;
   for (int s = 0; s < kMaxSlots; ++s) {
     Slot& sl = slots_[s];
     if (sl.state != SlotState::kActive || !sl.fresh) continue;
     if (!dyn_add(s) && sl.new_job) waiting_new = true;
   }
+  // the entries published together (one release after all of them): workgroups of a lingering launch that see them
+  // spread over all of them at once, where one at a time they would crowd onto the first and rebalance slowly
+  if (ctl_ != ctl0) __atomic_store_n(&d_.pmb->ctl, ctl_, __ATOMIC_RELEASE);
   if (adopted && waiting_new) yield_if_long();
 }
 
 // Publish the job of fresh slot s as a dynamic entry of the running launch (npow_internal.h
 // PoolDynEntry): exactly one launch in flight, enough of its budget left,
-// not yielded, a free ring position, an unbounded job with a full region left.  Its region is taken
+// not yielded, a free ring position, an unbounded job with a full region left, and either another live entry in it
+// (workgroups to move) or a lingering launch (its workgroups wait for one).  Its region is taken
 // from the job's queue as launch() would, and counts as part of the running launch.  Caller holds
-// g_pool.mu (adopt()).
+// g_pool.mu (adopt()), and releases PoolMailbox::ctl after its calls.
 bool Worker::dyn_add(int s) {
   Slot& sl = slots_[s];
   Job& j = *sl.job;
@@ -625,7 +660,7 @@ bool Worker::dyn_add(int s) {
   bool other = false;  // another live entry keeps the launch running (workgroups to move)
   for (int k = 0; k < kMaxSlots && !other; ++k)
     other = k != s && slots_[k].state == SlotState::kActive && !slots_[k].fresh;
-  if (!other) return false;  // they are leaving: the next launch, right after, takes the job
+  if (!other && !f.linger) return false;  // they are leaving: the next launch, right after, takes the job
   const double left_us = g_budget_us.load() - std::chrono::duration<double, std::micro>(
                                                   std::chrono::steady_clock::now() - front_start_).count();
   if (left_us < kDynMinUs) return false;  // the next launch, queued soon, takes it
@@ -653,13 +688,12 @@ bool Worker::dyn_add(int s) {
     if (j.t_launch == 0) j.t_launch = t;
     if (j.t_launch_dev[sl.k] == 0) j.t_launch_dev[sl.k] = t;
   }
-  ctl_ = (ctl_ & ~0xffffffffull) | (uint32_t)(ctl_ + 1);  // the low half wraps on its own
-  __atomic_store_n(&d_.pmb->ctl, ctl_, __ATOMIC_RELEASE);  // after the entry
+  ctl_ = (ctl_ & ~0xffffffffull) | (uint32_t)(ctl_ + 1);  // the low half wraps on its own (released by adopt())
   {
     std::lock_guard<std::mutex> sg(d_.stats_mu);
     d_.dyn++;
   }
-  NPOW_DBG("nanopow[%d]: dynamic entry %u: slot %d g%llu in launch %llu\n", d_.id, (uint32_t)ctl_ - 1u,
+  NPOW_DBGT("nanopow[%d]: dynamic entry %u: slot %d g%llu in launch %llu\n", d_.id, (uint32_t)ctl_ - 1u,
            s, (unsigned long long)sl.gen, (unsigned long long)f.seq);
   return true;
 }
@@ -916,6 +950,22 @@ void Worker::check_slots() {
   }
 }
 
+// No live entry in the launches in flight, and something waits for the device (a job that could not join them, a
+// sweep / values task, shutdown, a dropped device): a lingering launch would hold the device until its budget ends
+// (up to 20 ms), so end it now -- a yield (the high half of PoolMailbox::ctl), which its lingering workgroups read
+// within a look (ls2_linger) and which ends nothing else, no entry being live.  Raised before the next table is built
+// (launch() takes yield_base after it), so that launch is not ended too.
+void Worker::end_linger() {
+  bool lingering = false;
+  for (const PoolInflight& f : q_) lingering = lingering || (f.linger && (f.yield_base >> 32) == (ctl_ >> 32));
+  if (!lingering) return;
+  ctl_ += 1ull << 32;
+  __atomic_store_n(&d_.pmb->ctl, ctl_, __ATOMIC_RELEASE);
+  NPOW_DBGT("nanopow[%d]: lingering launch ended (ctl %llx)\n", d_.id, (unsigned long long)ctl_);
+  std::lock_guard<std::mutex> sg(d_.stats_mu);
+  d_.linger_ends++;
+}
+
 int Worker::launch() {
   if (q_.size() >= 2 || d_.dead) return NPOW_OK;
   // The second launch in flight only has to be queued before the running one ends (its budget
@@ -939,6 +989,7 @@ int Worker::launch() {
   for (int s = 0; s < kMaxSlots; ++s)
     if (slots_[s].state == SlotState::kActive && !slots_[s].no_more) idx[n++] = s;
   if (n == 0) return NPOW_OK;
+  if (!live_slot()) end_linger();  // (step() has raised it already when a job waits; a bounded range's next part)
   t.n = n;
   t.poll_mask = poll_mask();
   t.iters = iters;
@@ -947,8 +998,10 @@ int Worker::launch() {
   t.dyn_base = (uint32_t)ctl_;
   // One entry: the launch ends with it, and counting workgroups on it only delays that end (the
   // final count would reach the host ~60 us after the launch's own end; measured with
-  // NANOPOW_TRACE_LATENCY).  Two or more: a won entry's job need not wait for the others.
+  // NANOPOW_TRACE_LATENCY).  Two or more: a won entry's job need not wait for the others.  A lingering launch is
+  // counted from its first entry (set below, once the entries are known to be unbounded).
   t.counted = n >= 2 ? 1u : 0u;
+  t.linger = 0;
   t.kill_base = (uint32_t)__atomic_load_n(&d_.pmb->kills, __ATOMIC_ACQUIRE);
   ++seq_;
   t.ring = (uint32_t)ring_;
@@ -990,6 +1043,7 @@ int Worker::launch() {
       sl.fresh = false;
     }
   }
+  if (g_linger && !d_.time_shared && !bounded && g_budget_us.load() > 0) t.linger = t.counted = 1u;
   const int r = ring_;
   ring_ = (ring_ + 1) % kEventRing;
   const size_t bytes = pool_table_bytes(n);
@@ -1011,10 +1065,11 @@ int Worker::launch() {
   }
   HIPTRY(hipEventRecord(d_.ev_stop[r], d_.stream));
   if (q_.empty()) front_start_ = std::chrono::steady_clock::now();
-  NPOW_DBG("nanopow[%d]: launch %llu n=%u slots:", d_.id, (unsigned long long)seq_, n);
+  NPOW_DBGT("nanopow[%d]: launch %llu n=%u linger %u yield_base %llx slots:", d_.id, (unsigned long long)seq_, n,
+            t.linger, (unsigned long long)t.yield_base);
   for (uint32_t e = 0; e < n; ++e) NPOW_DBG(" %d/g%llu", idx[e], (unsigned long long)t.e[e].gen);
   NPOW_DBG("\n");
-  q_.push_back({seq_, r, (uint32_t)ctl_, t.yield_base, t.counted != 0});
+  q_.push_back({seq_, r, (uint32_t)ctl_, t.yield_base, t.counted != 0, t.linger != 0});
   return NPOW_OK;
 }
 
@@ -1070,6 +1125,14 @@ int Worker::retire() {
     prev_stop_ring_ = q_.front().ring;
     uint64_t g0 = 0, g1 = 0;
     account_clock(q_.front().ring, q_.front().seq, &g0, &g1);
+    if (g_trace_lat && g0) {  // the launch's event span against its clock waves' span (dispatch and drain)
+      float ev = 0.f;
+      if (hipEventElapsedTime(&ev, d_.ev_start[q_.front().ring], d_.ev_stop[q_.front().ring]) == hipSuccess)
+        fprintf(stderr, "nanopow-launch dev %d launch %llu: events %.1f clock waves %.1f us, start %.1f us after the "
+                "previous end\n", d_.id, (unsigned long long)q_.front().seq, ev * 1e3, (double)(g1 - g0) / 100.0,
+                prev_g1_ ? ((double)g0 - (double)prev_g1_) / 100.0 : -1.0);
+      prev_g1_ = g1;
+    }
     if (g_trace_lat && g0)  // GPU timeline of a decided job's launch on this device, from the deciding win (the same
                             // clock only for devices on one GPU: CU partitions)
       for (const Slot& sl : slots_)
@@ -1096,14 +1159,21 @@ int Worker::retire() {
       // its stop time is now (npow_wait_info), not when the done counts' read-back lands
       if (m > 0 && sl.inflight.empty() && sl.state == SlotState::kDraining && sl.job && sl.job->decided.load()) {
         std::lock_guard<std::mutex> g(g_pool.mu);
-        if (sl.job->t_stop[sl.k] == 0) sl.job->t_stop[sl.k] = now_us();
+        if (sl.job->t_stop[sl.k] == 0) {
+          sl.job->t_stop[sl.k] = now_us();
+          if (g_trace_lat)
+            fprintf(stderr, "nanopow-nofin dev %d ticket %llu slot %d g%llu: stopped at its launch's end, no final "
+                    "count (launch %llu, fin gen %llu)\n", d_.id, (unsigned long long)sl.job->ticket, s,
+                    (unsigned long long)sl.gen, (unsigned long long)seq,
+                    (unsigned long long)__atomic_load_n(&d_.pmb->fin[s].gen, __ATOMIC_ACQUIRE));
+        }
       }
     }
     if (g_trace_lat)
       for (Slot& sl : slots_)
         if (sl.state == SlotState::kDraining && sl.job && sl.job->t_win != 0 && sl.job->t_kend == 0)
           sl.job->t_kend = now_us();
-    NPOW_DBG("nanopow[%d]: launch %llu done\n", d_.id, (unsigned long long)q_.front().seq);
+    NPOW_DBGT("nanopow[%d]: launch %llu done\n", d_.id, (unsigned long long)q_.front().seq);
     retired_seq_ = q_.front().seq;
     q_.pop_front();
     front_start_ = std::chrono::steady_clock::now();  // the next one (if any) has just started
@@ -1203,6 +1273,19 @@ void Worker::fail_all(const std::string& msg) {
 int Worker::step() {
   timed(0, [&] { adopt(); return 0; });
   timed(1, [&] { check_slots(); return 0; });
+  if (!q_.empty() && !live_slot()) {
+    // a lingering launch idle for g_linger_us, or something waiting for the device, or its time budget over
+    const double t = now_us();
+    if (idle_since_ == 0) idle_since_ = t;
+    bool waiting = d_.tasks_waiting.load() > 0 || d_.dead || g_pool.stopping.load(std::memory_order_relaxed) ||
+                   t - idle_since_ > g_linger_us ||
+                   std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - front_start_).count() >
+                       (double)g_budget_us.load();
+    for (int s = 0; s < kMaxSlots && !waiting; ++s) waiting = slots_[s].state == SlotState::kActive;  // (fresh)
+    if (waiting) end_linger();
+  } else {
+    idle_since_ = 0;
+  }
   if (int rc = timed(2, [&] { return queue_readbacks(); })) return rc;  // before the next launch: it no longer holds them
   if (d_.tasks_waiting.load() == 0)                                       // a sweep / values call is waiting: drain instead
     if (int rc = timed(3, [&] { return launch(); })) return rc;
@@ -1374,6 +1457,7 @@ void pool_start() {
   {
     std::lock_guard<std::mutex> g(g_pool.mu);
     g_pool.running = true;
+    g_pool.stopping = false;
   }
   if (g_watcher_on) {
     {
@@ -1404,6 +1488,7 @@ void pool_stop() {
   {
     std::lock_guard<std::mutex> g(g_pool.mu);
     g_pool.running = false;
+    g_pool.stopping = true;  // workers end their lingering launches (end_linger)
     for (const JobP& j : g_pool.active) j->cancel_req = true;
     notify_workers_locked();
   }

@@ -79,6 +79,7 @@ struct Pool {
   uint64_t next_ticket = 1;
   uint32_t max_active = kMaxSlots;
   bool running = false;
+  std::atomic<bool> stopping{false};  // pool_stop: workers end their lingering launches at once
   std::atomic<uint64_t> version{0};  // bumped whenever `active` gains a job
   std::atomic<uint64_t> decisions{0};  // bumped when a job split over devices is decided: wakes napping workers
 };

@@ -32,6 +32,9 @@ class _Ticket:
     def wait(self, timeout=None):
         return self._res if self._ev.wait(timeout) else None
 
+    def cancel(self):
+        self._own.is_set = True
+
     def wait_result(self, timeout=None):  # the engine's npow_wait_result; here the outcome is the final result
         return self.wait(timeout)
 
@@ -64,7 +67,7 @@ class OracleEngine:
                                clock_mhz=0.0, early_finishes=0, kills_relayed=0, host_cpu_ms=0.0,
                                host_wall_ms=1.0, grid=0, pool_groups=4, late_nonces=0, hip_device=0,
                                cu_first=-1, cus=256, idle_ms=0.0, idle_gaps=0, affinity_checks=0, affinity_failures=0,
-                               watcher_decisions=0)
+                               watcher_decisions=0, dyn_entries=0)
 
     def version(self):
         return "oracle stand-in engine (tests/fake_engine.py)"
@@ -136,9 +139,14 @@ class OracleEngine:
                 time.sleep(self.delay)
 
     def submit(self, root, threshold, start=0, device_mask=0, max_nonces_per_device=0, cancel=None):
+        own = _Flag()  # Ticket.cancel() (npow_cancel)
+        either = _Either(own, cancel)
         if self.n_devices > 1 and not max_nonces_per_device:
-            return _Ticket(lambda: self._split(root, threshold, start, device_mask, cancel))
-        return _Ticket(lambda: self.search(root, threshold, start, device_mask, max_nonces_per_device, cancel))
+            tk = _Ticket(lambda: self._split(root, threshold, start, device_mask, either))
+        else:
+            tk = _Ticket(lambda: self.search(root, threshold, start, device_mask, max_nonces_per_device, either))
+        tk._own = own
+        return tk
 
 
 class _Either:

@@ -38,12 +38,17 @@ def run(name, spec, searches):
         return v["p50"] if isinstance(v, dict) and "p50" in v else None
     return {"arm": name, "devices": int(g), "node_over_kernel": r["node_over_kernel"], "node_gnps": r["node_gnps"],
             "kernel_gnps": r["kernel_gnps"], "fixed_us": r["fixed_cost_us"]["fixed_us"],
+            "reference_gnps": r.get("reference_gnps"), "node_over_reference": r.get("node_over_reference"),
+            "fixed_at_reference_us": r.get("fixed_cost_at_reference_us"),
+            "p50_minus_expected_at_reference_ms": r.get("p50_minus_expected_at_reference_ms"),
             "p50_ms": r["c_abi_ttw_ms"]["p50"], "p50_minus_expected_ms": r["p50_minus_expected_ms"],
             "idle_us": d["gpu_idle_between_launches"]["mean_per_gap"], "adopt_p50": p50("adopt"),
             "launch_last_p50": p50("launch_last_device"), "win_to_decided_p50": p50("win_seen_to_decided"),
             "decided_to_result_p50": p50("decided_to_result_in_client"),
             "turnaround_p50": p50("client_turnaround_to_next_submit"), "losers_stop_p50": p50("losers_stop_after_decide"),
-            "mhz": r["in_kernel_mhz"], "cores": r["worker_core_share"]}
+            "mhz": r["in_kernel_mhz"], "cores": r["worker_core_share"],
+            "launches_per_search": r.get("launches_per_search_per_device"),
+            "dyn_per_search": r.get("dyn_entries_per_search_per_device")}
 
 
 def main():
