@@ -227,12 +227,15 @@ struct alignas(64) PoolFin {
   uint8_t pad[24];
 };
 // An unbounded job adopted while a search launch runs joins that launch instead of ending it
-// (a yield): the host writes its entry at ring position p (dyn[p % kDynEntries]) and then releases
+// (a yield): the host writes its entry at ring position p (dyn[p % kDynRing]) and then releases
 // the low half of PoolMailbox::ctl = p + 1; the launch's entries are its table's n entries followed by positions
-// dyn_base.. of the ring, and workgroups move to a new entry as they rebalance (npow_kernel.hip).
-// Each entry has cache lines of its own, and a position is written at most once while a launch
-// that can read it runs, so no scalar-cache line can hold an older entry there.
+// dyn_base.. of the ring, at most kDynEntries of them, and workgroups move to a new entry as they rebalance
+// (npow_kernel.hip).  Each entry has cache lines of its own, and a position is written at most once while a launch
+// that can read it runs, so no scalar-cache line can hold an older entry there.  The ring holds two launches' worth
+// (round 5): a lingering launch whose kDynEntries are used up is replaced by an empty one queued behind it, and the
+// next search's entry goes to positions the ending launch cannot read (Worker::dyn_add).
 constexpr int kDynEntries = 32;
+constexpr int kDynRing = 2 * kDynEntries;
 struct alignas(64) PoolDynEntry {
   PoolEntry e;
   uint8_t pad[192 - sizeof(PoolEntry)];
@@ -241,7 +244,7 @@ static_assert(sizeof(PoolDynEntry) == 192, "3 cache lines per dynamic entry");
 struct PoolMailbox {
   PoolWin win[kMaxSlots];
   PoolFin fin[kMaxSlots];
-  PoolDynEntry dyn[kDynEntries];
+  PoolDynEntry dyn[kDynRing];
   uint64_t kill[kMaxSlots];  // kill[s] = gen: the job in slot s (that generation) must stop
   // High half: bumped by the host when new jobs wait for the next launch (a yield); low half: the
   // dynamic entries published (ring positions, see PoolDynEntry).  One word, so a poll reads both

@@ -555,7 +555,7 @@ constexpr uint32_t kNoEntry = 0xffffffffu;
 // and the table's and the ring's fields then load with scalar loads into SGPRs alike.
 typedef const __attribute__((address_space(4))) PoolEntry ConstEntry;
 __device__ __forceinline__ ConstEntry* ls2_entry(const PoolTable* tab, const PoolMailbox* mb, uint32_t e) {
-  const PoolEntry* p = e < tab->n ? &tab->e[e] : &mb->dyn[(tab->dyn_base + (e - tab->n)) % kDynEntries].e;
+  const PoolEntry* p = e < tab->n ? &tab->e[e] : &mb->dyn[(tab->dyn_base + (e - tab->n)) % kDynRing].e;
   return (ConstEntry*)(uintptr_t)p;
 }
 // Relaxed: an acquire at system scope invalidates the L2, which at every poll cost 4x the search
@@ -607,6 +607,10 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
                                          uint32_t* seen) {
   const ConstEntry* pe = ls2_entry(tab, mb, e);
   const uint64_t ctl = ls2_ctl(mb);
+  // a lingering launch keeps the device-memory mirror of ctl fresh from its polls too: a workgroup leaving an entry
+  // picks its next one from the mirror (ls2_pick), and the mirror is otherwise raised only by lingering workgroups
+  if (tab->linger)
+    __hip_atomic_fetch_max(&st->ctl_mirror[0], (unsigned long long)ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   // (a one-entry launch -- uncounted -- holds only the entry whose kill word this poll reads below: no read of
   // the counter there, whose uncached read at every poll was 0.76 MB per 10-ms launch of PMC traffic)
   // (nor in a launch of one entry so far: a lingering launch is counted from its first entry on)
@@ -640,9 +644,14 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
     __hip_atomic_store(kd, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if ((ctl >> 32) != (tab->yield_base >> 32)) {
+    // (only the entries still live: each kill is an atomic and, counted, 8 serial loads -- over a lingering launch's
+    // ring of 33 mostly finished entries ~0.35 ms, which held up a losing search's stop when the host ended the
+    // launch under it)
+    const unsigned long long over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
+      if ((over >> k) & 1) continue;
       ConstEntry* q = ls2_entry(tab, mb, k);
-      if (!q->bounded) ls2_kill(st, mb, q->slot, q->gen, tab->counted != 0);
+      if (!q->bounded && load_dead(st, q->slot) < q->gen) ls2_kill(st, mb, q->slot, q->gen, tab->counted != 0);
     }
     leave = !pe->bounded;
   }
@@ -809,7 +818,9 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     // a counted launch that held the same entry and has published its final count, after which no
     // nonce may be hashed for it (tests/test_gpu_configs.py caught one launch doing so).
     uint32_t first;
-    if (counted) {
+    if (n == 0) {
+      first = kNoEntry;  // an empty lingering launch (Worker::relaunch_linger): straight to ls2_linger
+    } else if (counted) {
       first = ls2_pick(tab, st, mb, g % n, true, &s_seen);
     } else {
       // only the device-side dead word: reading the pinned kill word here too (512 workgroups' PCIe reads

@@ -576,7 +576,7 @@ class Worker {
     d_.worker_busy.store(busy(), std::memory_order_release);
   }
   void check_slots();
-  int launch();
+  int launch(bool empty_linger = false);
   int queue_readbacks();
   int retire();
   void fail_all(const std::string& msg);
@@ -645,30 +645,38 @@ void Worker::adopt() {
 // Publish the job of fresh slot s as a dynamic entry of the running launch (npow_internal.h
 // PoolDynEntry): exactly one launch in flight, enough of its budget left,
 // not yielded, a free ring position, an unbounded job with a full region left, and either another live entry in it
-// (workgroups to move) or a lingering launch (its workgroups wait for one).  Its region is taken
-// from the job's queue as launch() would, and counts as part of the running launch.  Caller holds
-// g_pool.mu (adopt()), and releases PoolMailbox::ctl after its calls.
+// (workgroups to move) or a lingering launch (its workgroups wait for one).  Or (round 5) of the lingering launch
+// queued behind an ending one whose ring is used up (step(): the replacement), at positions the ending one cannot
+// read.  Its region is taken from the job's queue as launch() would, and counts as part of that launch.  Caller
+// holds g_pool.mu (adopt()), and releases PoolMailbox::ctl after its calls.
 bool Worker::dyn_add(int s) {
   Slot& sl = slots_[s];
   Job& j = *sl.job;
-  if (q_.size() != 1 || j.max_per_dev || g_budget_us.load() == 0) return false;
+  if (q_.empty() || q_.size() > 2 || j.max_per_dev || g_budget_us.load() == 0) return false;
   const PoolShape sh = pool_shape(d_);
-  const PoolInflight& f = q_.front();
+  const PoolInflight& f = q_.back();
   if (!f.counted) return false;  // a one-entry launch: the new job ends it (a yield) instead
   if ((uint32_t)((uint32_t)ctl_ - (uint32_t)f.dyn_base) >= (uint32_t)kDynEntries) return false;
   if ((ctl_ >> 32) != (f.yield_base >> 32)) return false;  // it is ending
-  bool other = false;  // another live entry keeps the launch running (workgroups to move)
-  for (int k = 0; k < kMaxSlots && !other; ++k)
-    other = k != s && slots_[k].state == SlotState::kActive && !slots_[k].fresh;
-  if (!other && !f.linger) return false;  // they are leaving: the next launch, right after, takes the job
-  const double left_us = g_budget_us.load() - std::chrono::duration<double, std::micro>(
-                                                  std::chrono::steady_clock::now() - front_start_).count();
-  if (left_us < kDynMinUs) return false;  // the next launch, queued soon, takes it
+  if (q_.size() == 2) {
+    // the queued launch: a lingering one behind a launch that cannot see its ring positions (its own kDynEntries
+    // were used up before this one was built: ring positions dyn_base .. dyn_base + kDynEntries - 1 of each, and
+    // the ring holds both); it starts as soon as the other one's workgroups have left
+    if (!f.linger || (uint32_t)(f.dyn_base - (uint32_t)q_.front().dyn_base) < (uint32_t)kDynEntries) return false;
+  } else {
+    bool other = false;  // another live entry keeps the launch running (workgroups to move)
+    for (int k = 0; k < kMaxSlots && !other; ++k)
+      other = k != s && slots_[k].state == SlotState::kActive && !slots_[k].fresh;
+    if (!other && !f.linger) return false;  // they are leaving: the next launch, right after, takes the job
+    const double left_us = g_budget_us.load() - std::chrono::duration<double, std::micro>(
+                                                    std::chrono::steady_clock::now() - front_start_).count();
+    if (left_us < kDynMinUs) return false;  // the next launch, queued soon, takes it
+  }
   const uint32_t iters = sh.launch_iters(g_iters.load());
   const uint64_t full = sh.full(iters);
   std::deque<Range>& todo = j.todo[sl.k];
   if (todo.empty() || todo.front().count < full) return false;
-  PoolEntry& pe = d_.pmb->dyn[(uint32_t)ctl_ % kDynEntries].e;
+  PoolEntry& pe = d_.pmb->dyn[(uint32_t)ctl_ % kDynRing].e;
   memcpy(pe.u, j.u, sizeof(pe.u));
   pe.threshold = j.threshold;
   pe.gen = sl.gen;
@@ -873,8 +881,8 @@ void Worker::early_finish(int s) {
   Job& j = *sl.job;
   if (g_trace_lat && j.gpu_t_win) {  // GPU timeline (one GPU's clock: CU partitions), from the deciding win
     const double tw = (double)j.gpu_t_win, tr = (double)__atomic_load_n(&d_.pmb->fin[s].t_relay, __ATOMIC_RELAXED);
-    fprintf(stderr, "nanopow-fin dev %d ticket %llu: relay %+.1f fin %+.1f seen %+.1f us (host) from the win%s\n", d_.id,
-            (unsigned long long)j.ticket, (tr - tw) / 100.0,
+    fprintf(stderr, "[%.3f] nanopow-fin dev %d ticket %llu: relay %+.1f fin %+.1f seen %+.1f us (host) from the win%s\n",
+            now_us() * 1e-3, d_.id, (unsigned long long)j.ticket, (tr - tw) / 100.0,
             ((double)__atomic_load_n(&d_.pmb->fin[s].t_fin, __ATOMIC_RELAXED) - tw) / 100.0,
             j.t_win_seen > 0 ? now_us() - j.t_win_seen : -1.0, (int)sl.k == j.winner_k ? " (winner)" : "");
   }
@@ -966,7 +974,7 @@ void Worker::end_linger() {
   d_.linger_ends++;
 }
 
-int Worker::launch() {
+int Worker::launch(bool empty_linger) {
   if (q_.size() >= 2 || d_.dead) return NPOW_OK;
   // The second launch in flight only has to be queued before the running one ends (its budget
   // is known): queued early, it would sit behind a launch that a win ends, and the job could
@@ -988,7 +996,7 @@ int Worker::launch() {
   int idx[kMaxSlots];
   for (int s = 0; s < kMaxSlots; ++s)
     if (slots_[s].state == SlotState::kActive && !slots_[s].no_more) idx[n++] = s;
-  if (n == 0) return NPOW_OK;
+  if (n == 0 && !empty_linger) return NPOW_OK;
   if (!live_slot()) end_linger();  // (step() has raised it already when a job waits; a bounded range's next part)
   t.n = n;
   t.poll_mask = poll_mask();
@@ -1044,6 +1052,7 @@ int Worker::launch() {
     }
   }
   if (g_linger && !d_.time_shared && !bounded && g_budget_us.load() > 0) t.linger = t.counted = 1u;
+  if (n == 0 && !t.linger) return NPOW_OK;
   const int r = ring_;
   ring_ = (ring_ + 1) % kEventRing;
   const size_t bytes = pool_table_bytes(n);
@@ -1157,7 +1166,11 @@ int Worker::retire() {
       sl.inflight.erase(sl.inflight.begin(), sl.inflight.begin() + (ptrdiff_t)m);
       // a decided job's last launch on this device has completed: the device hashes nothing more of it, so
       // its stop time is now (npow_wait_info), not when the done counts' read-back lands
-      if (m > 0 && sl.inflight.empty() && sl.state == SlotState::kDraining && sl.job && sl.job->decided.load()) {
+      // (a slot finished from its final count has its stop time already: no pool lock for it -- a lingering launch
+      // retires with up to 33 of them, and 33 acquisitions of the contended lock held up this worker's next look at
+      // a live search by up to ~0.1 ms)
+      if (m > 0 && sl.inflight.empty() && sl.state == SlotState::kDraining && !sl.early && sl.job &&
+          sl.job->decided.load()) {
         std::lock_guard<std::mutex> g(g_pool.mu);
         if (sl.job->t_stop[sl.k] == 0) {
           sl.job->t_stop[sl.k] = now_us();
@@ -1274,15 +1287,30 @@ int Worker::step() {
   timed(0, [&] { adopt(); return 0; });
   timed(1, [&] { check_slots(); return 0; });
   if (!q_.empty() && !live_slot()) {
-    // a lingering launch idle for g_linger_us, or something waiting for the device, or its time budget over
+    // a lingering launch idle for g_linger_us, or something waiting for the device, or its time budget over.  Idle
+    // means also no won or killed slot still draining in it (its final count not in): ended under such a slot, the
+    // launch's yield would race the kill relay (npow_kernel.hip ls2_poll)
+    bool draining = false;
+    for (const Slot& sl : slots_)
+      draining = draining || (sl.state == SlotState::kDraining && !sl.fin_seen && !sl.inflight.empty());
     const double t = now_us();
-    if (idle_since_ == 0) idle_since_ = t;
+    if (idle_since_ == 0 && !draining) idle_since_ = t;
     bool waiting = d_.tasks_waiting.load() > 0 || d_.dead || g_pool.stopping.load(std::memory_order_relaxed) ||
-                   t - idle_since_ > g_linger_us ||
+                   (idle_since_ > 0 && t - idle_since_ > g_linger_us) ||
                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - front_start_).count() >
                        (double)g_budget_us.load();
     for (int s = 0; s < kMaxSlots && !waiting; ++s) waiting = slots_[s].state == SlotState::kActive;  // (fresh)
-    if (waiting) end_linger();
+    if (waiting) {
+      end_linger();
+    } else if (!draining && q_.size() == 1 && q_.front().linger && d_.tasks_waiting.load() == 0 &&
+               (uint32_t)((uint32_t)ctl_ - (uint32_t)q_.front().dyn_base) >= (uint32_t)kDynEntries) {
+      // idle, and its dynamic entries used up: the next search could not join it, and would wait for it to end and
+      // for a launch of its own (0.1-0.7 ms over 8 CU partitions, every 33rd search of a serial client).  End it now
+      // and queue an empty lingering launch behind it, whose workgroups take the CUs as its own leave; the next
+      // search joins that one (dyn_add), in ring positions the ending launch does not read.
+      end_linger();
+      if (int rc = timed(3, [&] { return launch(true); })) return rc;
+    }
   } else {
     idle_since_ = 0;
   }
