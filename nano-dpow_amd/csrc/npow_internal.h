@@ -131,9 +131,10 @@ struct PoolTable {
                           // launch with one entry ends with it, and counting only slows its end.
   uint32_t kill_base;     // the low half of PoolMailbox::kills when the table was built: a polling wave that
                           // reads another value relays the kill words of every entry, not only its own
-  uint32_t linger;        // search kernels (counted launches, round 5): a workgroup that finds no live entry waits
-                          // in the launch for the host's next dynamic entry (ls2_linger) until the time budget
-                          // ends or a yield, instead of leaving -- the next search needs no launch
+  uint32_t linger;        // search kernels (counted launches, round 5), > 0: a workgroup that finds no live entry
+                          // waits in the launch for the host's next dynamic entry (ls2_linger) until a yield,
+                          // instead of leaving -- the next search needs no launch; the value (a power of two) is
+                          // the lingering workgroups' period, in looks, of reading the pinned ctl word
   uint32_t pad[4];
   PoolEntry e[kMaxSlots];
 };
@@ -195,6 +196,11 @@ struct PoolDevState {
   // lingering workgroups to read from device memory: one uncached host read per 64 lingering workgroups' looks
   // instead of one each.  Monotonic like ctl; a value older than a launch's table reads as no news (ls2_mirror_ok).
   alignas(64) unsigned long long ctl_mirror[8];
+  // Per XCD (hardware XCC id): the dynamic-entry count (the low half of PoolMailbox::ctl, absolute) up to which a
+  // workgroup on that XCD has invalidated its L2 after seeing the entries published (ls2_fresh): one invalidation
+  // per XCD and entry instead of one per workgroup (round 5).  One line each.
+  alignas(64) unsigned int xcd_acq[8][16];
+  alignas(64) unsigned int xcd_claim[8][16];  // ... and the count some workgroup of the XCD has taken the job for
 };
 
 // Pinned host-coherent mailbox of the pool: one win record per slot (the winner stores
@@ -224,7 +230,8 @@ struct alignas(64) PoolFin {
   uint64_t late;   // the slot's late words, summed (kLateWord; cumulative)
   uint64_t t_fin;    // s_memrealtime of the publication (NANOPOW_TRACE_LATENCY GPU timelines)
   uint64_t t_relay;  // diagnostic builds (-DNPOW_DIAG_TIMES): s_memrealtime when a poll read the slot's kill word
-  uint8_t pad[24];
+  uint64_t t_join;   // ... and when a workgroup last started hashing the slot's entry
+  uint8_t pad[16];
 };
 // An unbounded job adopted while a search launch runs joins that launch instead of ending it
 // (a yield): the host writes its entry at ring position p (dyn[p % kDynRing]) and then releases
@@ -254,6 +261,9 @@ struct PoolMailbox {
   // and with n live entries a kill of another entry would wait ~n polls for a wave on that entry.
   alignas(64) uint64_t kills;
   alignas(64) PoolClk clk[kPoolRing][kClkWaves];  // [launch ring][XCD] (host: kEventRing == kPoolRing)
+#ifdef NPOW_DIAG_TIMES
+  uint64_t diag_join[1024];  // diagnostic builds: s_memrealtime when workgroup g last started an entry
+#endif
 };
 
 // Grid of a search launch: kLsGroups 512-lane workgroups per CU.  A "unit" is what an entry's share

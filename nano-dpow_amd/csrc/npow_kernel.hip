@@ -565,9 +565,47 @@ __device__ __forceinline__ ConstEntry* ls2_entry(const PoolTable* tab, const Poo
 __device__ __forceinline__ uint64_t ls2_ctl(PoolMailbox* mb) {
   return __hip_atomic_load(&mb->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__device__ __forceinline__ void ls2_fresh(uint32_t nd, uint32_t* seen) {
+// The L2 is per XCD, so one workgroup per XCD and entry invalidates it (round 5: a lingering launch's 1,024 workgroups
+// all joining the next search's entry each invalidated their XCD's L2, 128 invalidations per XCD one after another:
+// the last workgroup started hashing ~0.2 ms after the first).  The one that does raises PoolDevState::xcd_acq after
+// its invalidation has completed; a workgroup that finds it raised far enough reads the entries from an L2 that has
+// been invalidated after they were written (a line filled since was read from host memory after the write).
+__device__ __forceinline__ uint32_t xcc_id() {
+  uint32_t x;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+  return x & 7u;
+}
+__device__ __forceinline__ void ls2_fresh(const PoolTable* tab, PoolDevState* st, uint32_t nd, uint32_t* seen) {
   if (nd > *seen) {
-    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the host wrote the entries
+    // (one lane decides: ls2_choose calls this with the whole wave, ls2_poll with lane 0 alone -- a claim made by
+    // every lane would have one lane invalidating and the others waiting for it in the same divergent wave)
+    const uint32_t want = tab->dyn_base + nd, x = xcc_id();
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    unsigned int* const acq = &st->xcd_acq[x][0];
+    uint32_t role = 0;  // 0: this XCD's L2 is fresh already, 1: invalidate it, 2: wait for the workgroup that does
+    if (lane == __builtin_amdgcn_readfirstlane(lane)) {
+      if ((int32_t)(__hip_atomic_load(acq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
+        // the first workgroup of the XCD to get here invalidates; the others wait for it (a workgroup per XCD and
+        // entry: ~128 arrive within a few microseconds, and letting each that found acq behind invalidate too
+        // serialised most of them again)
+        const unsigned int was =
+            __hip_atomic_fetch_max(&st->xcd_claim[x][0], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        role = (int32_t)(was - want) < 0 ? 1u : 2u;
+      }
+    }
+    role = __builtin_amdgcn_readfirstlane(role);
+    if (role == 1u) {
+#ifndef NPOW_DIAG_NO_FRESH_FENCE
+      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the host wrote the entries
+#endif
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidation has completed
+      if (lane == __builtin_amdgcn_readfirstlane(lane))
+        __hip_atomic_fetch_max(acq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if (role == 2u) {
+      while ((int32_t)(__builtin_amdgcn_readfirstlane(
+                           __hip_atomic_load(acq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - want) < 0)
+        __builtin_amdgcn_s_sleep(2);
+    }
     *seen = nd;
   }
 }
@@ -618,7 +656,7 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
   const uint32_t kills = tab->counted && tab->n + nd > 1
                              ? (uint32_t)__hip_atomic_load(&mb->kills, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                              : tab->kill_base;
-  ls2_fresh(nd, seen);
+  ls2_fresh(tab, st, nd, seen);
   bool leave = false;
   // A job of this launch was killed since it was built, and no wave has relayed that kill yet: relay every such
   // entry (its dead word first, a device read; the kill word, uncached, only for live entries), then record the
@@ -688,7 +726,7 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
 __device__ __forceinline__ uint32_t ls2_choose(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t e,
                                                uint32_t nd, uint32_t* seen, uint32_t lane, uint32_t g) {
   const uint32_t N = tab->n + nd;  // <= kMaxSlots = 64: one lane each
-  ls2_fresh(nd, seen);
+  ls2_fresh(tab, st, nd, seen);
   for (int attempt = 0; attempt < 4; ++attempt) {
     unsigned long long key = ~0ull;
     bool over = false;
@@ -734,9 +772,8 @@ __device__ __forceinline__ uint32_t ls2_choose(const PoolTable* tab, PoolDevStat
 __device__ __forceinline__ uint32_t ls2_linger(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t* seen,
                                             uint32_t looked) {
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-  const uint32_t g = blockIdx.x, G = gridDim.x;
-  uint32_t P = 1;
-  while (P * 2 < G) P <<= 1;
+  const uint32_t g = blockIdx.x;
+  const uint32_t P = tab->linger;  // a power of two (Worker::launch)
   unsigned long long* const mirror = &st->ctl_mirror[0];
   const uint32_t base_hi = (uint32_t)(tab->yield_base >> 32);
   const uint32_t t_enter = (uint32_t)__builtin_amdgcn_s_memrealtime();
@@ -845,6 +882,13 @@ __device__ __forceinline__ void pool_body_ls2(const PoolTable* __restrict__ tab,
     const PoolEntry* pe = (const PoolEntry*)ls2_entry(tab, mb, e);
     PoolCursor c;
     pool_load_ls(pe, c, g, wv, G, n, e, iters);
+#ifdef NPOW_DIAG_TIMES
+    if (wv == 0 && lane == 0) {
+      const uint64_t tj = __builtin_amdgcn_s_memrealtime();
+      __hip_atomic_store(&mb->fin[c.slot].t_join, tj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->diag_join[g & 1023], tj, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+#endif
     // the poll phase restarts with each entry: the workgroups that join one together (a launch's start, a lingering
     // launch's next search) then hash it in step, so exactly one wave in poll_mask + 1 polls per iteration; carried
     // on from the launch's start instead, the phases of workgroups that had lingered apart drifted and the polls

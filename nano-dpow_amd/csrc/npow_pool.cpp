@@ -91,6 +91,12 @@ const bool g_linger = [] {
   const char* e = getenv("NANOPOW_LINGER");
   return !(e && e[0] == '0');
 }();
+const uint32_t g_linger_p = [] {  // NANOPOW_LINGER_P (A/B runs): the pinned-read period in looks (a power of two)
+  const char* e = getenv("NANOPOW_LINGER_P");
+  uint32_t p = e ? (uint32_t)atoi(e) : 0u, q = 1;
+  while (p && q < p) q <<= 1;
+  return p ? q : 0u;
+}();
 const double g_linger_us = [] {
   const char* e = getenv("NANOPOW_LINGER_US");
   return e ? atof(e) : 1000.0;
@@ -885,6 +891,23 @@ void Worker::early_finish(int s) {
             now_us() * 1e-3, d_.id, (unsigned long long)j.ticket, (tr - tw) / 100.0,
             ((double)__atomic_load_n(&d_.pmb->fin[s].t_fin, __ATOMIC_RELAXED) - tw) / 100.0,
             j.t_win_seen > 0 ? now_us() - j.t_win_seen : -1.0, (int)sl.k == j.winner_k ? " (winner)" : "");
+#ifdef NPOW_DIAG_TIMES
+    // absolute GPU times (100 MHz) of this entry's last start and its win, host times (us) of its launch / dynamic
+    // entry and of its win seen: a serial client's gap between one search's win and the next one's hashing
+    fprintf(stderr, "nanopow-join dev %d ticket %llu: gpu_join %llu gpu_win %llu host_launch %.1f host_win_seen %.1f\n",
+            d_.id, (unsigned long long)j.ticket,
+            (unsigned long long)__atomic_load_n(&d_.pmb->fin[s].t_join, __ATOMIC_RELAXED),
+            (unsigned long long)j.gpu_t_win, j.t_launch_dev[sl.k], j.t_win_seen);
+    {  // every workgroup's last entry start (a serial client: this search's) -- its spread
+      std::vector<uint64_t> tj;
+      const int G = ls_grid(d_) < 1024 ? ls_grid(d_) : 1024;
+      for (int g = 0; g < G; ++g) tj.push_back(__atomic_load_n(&d_.pmb->diag_join[g], __ATOMIC_RELAXED));
+      std::sort(tj.begin(), tj.end());
+      fprintf(stderr, "nanopow-joins dev %d ticket %llu: min %llu p10 %llu p50 %llu p90 %llu max %llu\n", d_.id,
+              (unsigned long long)j.ticket, (unsigned long long)tj[0], (unsigned long long)tj[G / 10],
+              (unsigned long long)tj[G / 2], (unsigned long long)tj[G * 9 / 10], (unsigned long long)tj[G - 1]);
+    }
+#endif
   }
   if (d_.dead || sl.requeue || !j.decided.load()) return;
   sl.early = true;
@@ -1051,7 +1074,14 @@ int Worker::launch(bool empty_linger) {
       sl.fresh = false;
     }
   }
-  if (g_linger && !d_.time_shared && !bounded && g_budget_us.load() > 0) t.linger = t.counted = 1u;
+  if (g_linger && !d_.time_shared && !bounded && g_budget_us.load() > 0) {
+    // each lingering workgroup reads the pinned ctl word once in P looks (phase g): ~2 reads per look grid-wide
+    uint32_t P = 1;
+    while (P * 2 < (uint32_t)sh.grid) P <<= 1;
+    if (g_linger_p > 0) P = g_linger_p;
+    t.linger = P;
+    t.counted = 1u;
+  }
   if (n == 0 && !t.linger) return NPOW_OK;
   const int r = ring_;
   ring_ = (ring_ + 1) % kEventRing;
