@@ -196,11 +196,6 @@ struct PoolDevState {
   // lingering workgroups to read from device memory: one uncached host read per 64 lingering workgroups' looks
   // instead of one each.  Monotonic like ctl; a value older than a launch's table reads as no news (ls2_mirror_ok).
   alignas(64) unsigned long long ctl_mirror[8];
-  // Per XCD (hardware XCC id): the dynamic-entry count (the low half of PoolMailbox::ctl, absolute) up to which a
-  // workgroup on that XCD has invalidated its L2 after seeing the entries published (ls2_fresh): one invalidation
-  // per XCD and entry instead of one per workgroup (round 5).  One line each.
-  alignas(64) unsigned int xcd_acq[8][16];
-  alignas(64) unsigned int xcd_claim[8][16];  // ... and the count some workgroup of the XCD has taken the job for
 };
 
 // Pinned host-coherent mailbox of the pool: one win record per slot (the winner stores

@@ -558,6 +558,25 @@ __device__ __forceinline__ ConstEntry* ls2_entry(const PoolTable* tab, const Poo
   const PoolEntry* p = e < tab->n ? &tab->e[e] : &mb->dyn[(tab->dyn_base + (e - tab->n)) % kDynRing].e;
   return (ConstEntry*)(uintptr_t)p;
 }
+// An entry's slot, generation and bounded flag for a poll's scans of the launch's other entries (kill relays, yields,
+// balancing).  A dynamic entry's are read past the caches (system-scope loads of host memory), so a poll needs no
+// acquire of newly published entries first (ls2_fresh: an L2 invalidation, one per XCD, the others waiting for it --
+// a poll that waited there held up its workgroup's stop when a search was won); a workgroup that picks an entry to
+// hash does acquire (ls2_choose).
+struct EntryHdr {
+  uint64_t gen;
+  uint32_t slot, bounded;
+};
+__device__ __forceinline__ EntryHdr ls2_hdr(const PoolTable* tab, PoolMailbox* mb, uint32_t e) {
+  if (e < tab->n) {
+    ConstEntry* q = (ConstEntry*)(uintptr_t)&tab->e[e];
+    return EntryHdr{q->gen, q->slot, q->bounded};
+  }
+  PoolEntry* q = &mb->dyn[(tab->dyn_base + (e - tab->n)) % kDynRing].e;
+  return EntryHdr{__hip_atomic_load(&q->gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                  __hip_atomic_load(&q->slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                  __hip_atomic_load(&q->bounded, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)};
+}
 // Relaxed: an acquire at system scope invalidates the L2, which at every poll cost 4x the search
 // kernel's fetches.  But a ring position's lines may still sit in an XCD's L2 from an earlier launch
 // (measured: wrong uniforms, invalid work), so a workgroup acquires once after it first sees a newly
@@ -565,47 +584,17 @@ __device__ __forceinline__ ConstEntry* ls2_entry(const PoolTable* tab, const Poo
 __device__ __forceinline__ uint64_t ls2_ctl(PoolMailbox* mb) {
   return __hip_atomic_load(&mb->ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-// The L2 is per XCD, so one workgroup per XCD and entry invalidates it (round 5: a lingering launch's 1,024 workgroups
-// all joining the next search's entry each invalidated their XCD's L2, 128 invalidations per XCD one after another:
-// the last workgroup started hashing ~0.2 ms after the first).  The one that does raises PoolDevState::xcd_acq after
-// its invalidation has completed; a workgroup that finds it raised far enough reads the entries from an L2 that has
-// been invalidated after they were written (a line filled since was read from host memory after the write).
-__device__ __forceinline__ uint32_t xcc_id() {
-  uint32_t x;
-  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
-  return x & 7u;
-}
+// Each workgroup acquires for itself (round 5 tried one L2 invalidation per XCD with the others waiting for it, and an
+// L1 invalidation each: the waits and the L1s made the joins as slow, and a skipped L1 invalidation let picks read
+// stale generations -- tools/gpu_r05ac.sh, r05ad).  Only picks acquire: polls read other entries past the caches
+// (ls2_hdr).
 __device__ __forceinline__ void ls2_fresh(const PoolTable* tab, PoolDevState* st, uint32_t nd, uint32_t* seen) {
+  (void)tab;
+  (void)st;
   if (nd > *seen) {
-    // (one lane decides: ls2_choose calls this with the whole wave, ls2_poll with lane 0 alone -- a claim made by
-    // every lane would have one lane invalidating and the others waiting for it in the same divergent wave)
-    const uint32_t want = tab->dyn_base + nd, x = xcc_id();
-    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-    unsigned int* const acq = &st->xcd_acq[x][0];
-    uint32_t role = 0;  // 0: this XCD's L2 is fresh already, 1: invalidate it, 2: wait for the workgroup that does
-    if (lane == __builtin_amdgcn_readfirstlane(lane)) {
-      if ((int32_t)(__hip_atomic_load(acq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - want) < 0) {
-        // the first workgroup of the XCD to get here invalidates; the others wait for it (a workgroup per XCD and
-        // entry: ~128 arrive within a few microseconds, and letting each that found acq behind invalidate too
-        // serialised most of them again)
-        const unsigned int was =
-            __hip_atomic_fetch_max(&st->xcd_claim[x][0], want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        role = (int32_t)(was - want) < 0 ? 1u : 2u;
-      }
-    }
-    role = __builtin_amdgcn_readfirstlane(role);
-    if (role == 1u) {
 #ifndef NPOW_DIAG_NO_FRESH_FENCE
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the host wrote the entries
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);  // system scope: the host wrote the entries
 #endif
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the invalidation has completed
-      if (lane == __builtin_amdgcn_readfirstlane(lane))
-        __hip_atomic_fetch_max(acq, want, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else if (role == 2u) {
-      while ((int32_t)(__builtin_amdgcn_readfirstlane(
-                           __hip_atomic_load(acq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) - want) < 0)
-        __builtin_amdgcn_s_sleep(2);
-    }
     *seen = nd;
   }
 }
@@ -656,7 +645,7 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
   const uint32_t kills = tab->counted && tab->n + nd > 1
                              ? (uint32_t)__hip_atomic_load(&mb->kills, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
                              : tab->kill_base;
-  ls2_fresh(tab, st, nd, seen);
+  (void)seen;  // (the entries it looks at here are read past the caches: ls2_hdr)
   bool leave = false;
   // A job of this launch was killed since it was built, and no wave has relayed that kill yet: relay every such
   // entry (its dead word first, a device read; the kill word, uncached, only for live entries), then record the
@@ -674,10 +663,10 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
     const unsigned long long over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
       if ((over >> k) & 1) continue;
-      ConstEntry* q = ls2_entry(tab, mb, k);
-      if (load_dead(st, q->slot) < q->gen &&
-          __hip_atomic_load(&mb->kill[q->slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q->gen)
-        ls2_kill(st, mb, q->slot, q->gen, tab->counted != 0);
+      const EntryHdr q = ls2_hdr(tab, mb, k);
+      if (load_dead(st, q.slot) < q.gen &&
+          __hip_atomic_load(&mb->kill[q.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q.gen)
+        ls2_kill(st, mb, q.slot, q.gen, tab->counted != 0);
     }
     __hip_atomic_store(kd, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -688,8 +677,8 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
     const unsigned long long over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     for (uint32_t k = 0; k < tab->n + nd; ++k) {
       if ((over >> k) & 1) continue;
-      ConstEntry* q = ls2_entry(tab, mb, k);
-      if (!q->bounded && load_dead(st, q->slot) < q->gen) ls2_kill(st, mb, q->slot, q->gen, tab->counted != 0);
+      const EntryHdr q = ls2_hdr(tab, mb, k);
+      if (!q.bounded && load_dead(st, q.slot) < q.gen) ls2_kill(st, mb, q.slot, q.gen, tab->counted != 0);
     }
     leave = !pe->bounded;
   }
@@ -708,12 +697,12 @@ __device__ __forceinline__ uint32_t ls2_poll(const PoolTable* tab, PoolDevState*
     unsigned long long found = 0;
     for (uint32_t k = tab->n; k < tab->n + nd && !leave; ++k) {
       if (k == e || ((over >> k) & 1)) continue;
-      ConstEntry* q = ls2_entry(tab, mb, k);
-      if (q->bounded || load_dead(st, q->slot) >= q->gen) {
+      const EntryHdr q = ls2_hdr(tab, mb, k);
+      if (q.bounded || load_dead(st, q.slot) >= q.gen) {
         found |= 1ull << k;
         continue;
       }
-      leave = ls2_wgs(st, q->slot) + 2 <= mine;
+      leave = ls2_wgs(st, q.slot) + 2 <= mine;
     }
     ls2_mark_over(found);
   }

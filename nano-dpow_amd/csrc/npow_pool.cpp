@@ -85,12 +85,16 @@ const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
 // Lingering launches (round 5, PoolTable::linger): an unbounded launch's workgroups wait in it for the next dynamic
 // entry once its entries are over, so a serial client's next search joins the running launch instead of needing one.
 // The worker ends a launch that has lingered g_linger_us with nothing to do (end_linger): its sleeping waves hold the
-// CUs, and a serial client's next search comes within ~0.1 ms.  NANOPOW_LINGER=0 turns it off (A/B runs),
-// NANOPOW_LINGER_US sets the wait.  Off for logical devices that time-share a GPU (Device::time_shared).
-const bool g_linger = [] {
+// CUs, and a serial client's next search comes within ~0.1 ms.  Measured: over 8 CU partitions
+// the 2^26-nonce regime's node rate 0.95 -> 0.985-0.99 of the devices' full rate, on one device no gain (0.99-1.0
+// either way, the bench -0.1 to -0.3 %: each workgroup's acquire of a new entry spreads their start).  So by default
+// on when the pool has 2 or more GPU devices (pool_start); NANOPOW_LINGER=1 / 0 forces it on / off, NANOPOW_LINGER_US
+// sets the wait.  Never for logical devices that time-share a GPU (Device::time_shared).
+const int g_linger_env = [] {
   const char* e = getenv("NANOPOW_LINGER");
-  return !(e && e[0] == '0');
+  return e ? (e[0] == '0' ? 0 : 1) : -1;
 }();
+bool g_linger = false;  // pool_start
 const uint32_t g_linger_p = [] {  // NANOPOW_LINGER_P (A/B runs): the pinned-read period in looks (a power of two)
   const char* e = getenv("NANOPOW_LINGER_P");
   uint32_t p = e ? (uint32_t)atoi(e) : 0u, q = 1;
@@ -1517,6 +1521,9 @@ void pool_start() {
     g_pool.running = true;
     g_pool.stopping = false;
   }
+  int gpus = 0;
+  for (auto& d : g_devs) gpus += d->cpu_threads == 0 ? 1 : 0;
+  g_linger = g_linger_env >= 0 ? g_linger_env == 1 : gpus >= 2;
   if (g_watcher_on) {
     {
       std::lock_guard<std::mutex> g(g_watch.mu);

@@ -1,147 +1,143 @@
 """Lingering launches (round 5, npow_kernel.hip ls2_linger; npow_pool.cpp Worker::end_linger): a search launch whose
 entries are over waits in the GPU for the host's next dynamic entry, so a serial client's next root needs no launch.
+On by default when the pool has 2 or more GPU devices, forced on / off with NANOPOW_LINGER=1 / 0 -- so every case
+runs in a child process with its own environment.
 
 Checked here: serial searches reuse launches (fewer launches than searches, the rest joined as dynamic entries) and
-every result re-validates under hashlib; the nonce counts still add up to the device counter; a sweep, a values call
-and a bounded search right after a search do not wait for the lingering launch's time budget (20 ms); the launch
-ends on its own once idle; NANOPOW_LINGER=0 gives one launch per search; split searches over CU partitions.
+every result re-validates under hashlib; the nonce counts still add up to the device counters; a sweep, a values call
+and a bounded search right after a search do not wait for the lingering launch's time budget (20 ms); an idle launch
+ends on its own; the defaults (one device: off, CU partitions: on); time-shared logical devices never linger.
 Run on an MI355X: ``pytest -m gpu``.
 """
 import json
 import os
-import random
 import subprocess
 import sys
-import time
 
 import pytest
 
-import oracle
 from conftest import ROOT
-from nanopow import _lib
 
 pytestmark = pytest.mark.gpu
-RECEIVE, LOW = 0xfffffe0000000000, 0xfffff00000000000
 
-
-def _roots(seed, n):
+PRELUDE = r"""
+import json, random, sys, time
+sys.path.insert(0, "nano-dpow_amd"); sys.path.insert(0, "oracle")
+import nanopow, oracle
+from nanopow import _lib
+eng = nanopow.engine()
+G = eng.n_devices
+MASK = (1 << G) - 1
+RECEIVE = 0xfffffe0000000000
+def roots(seed, n):
     rng = random.Random(seed)
     return [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(n)]
-
-
-def _serial(eng, roots, thr, mask=1):
+def serial(rs, thr=RECEIVE, mask=MASK):
     done = 0
-    for i, r in enumerate(roots):
+    for i, r in enumerate(rs):
         res = eng.submit(r, thr, start=i << 40, device_mask=mask).wait(30)
         assert res is not None and res.status == _lib.NPOW_OK, i
         assert oracle.work_value_hashlib(r, res.nonce) == res.value >= thr, i
         done += res.nonces_done
     return done
-
-
-def test_serial_searches_join_the_lingering_launch(gpu_engine):
-    time.sleep(0.05)  # an earlier test's lingering launch ends on its own (budget)
-    gpu_engine.reset_stats(0)
-    roots = _roots(51, 300)
-    done = _serial(gpu_engine, roots, RECEIVE)
-    st = gpu_engine.stats(0)
-    # ~0.2 ms per search: a 20-ms launch serves its table entry and up to 32 dynamic entries
-    assert st.launches < len(roots) // 4, (st.launches, st.dyn_entries)
-    assert st.dyn_entries >= len(roots) // 2, (st.launches, st.dyn_entries)
-    assert st.nonces == done
-    assert st.early_mismatches == 0
-
-
-def test_a_sweep_after_a_search_does_not_wait_for_the_budget(gpu_engine):
-    root = _roots(52, 1)[0]
-    gpu_engine.sweep(root, 0xffffffc000000000, 0, 1 << 22, device_mask=1)  # the first call loads the kernel (~20 ms)
-    for trial in range(3):
-        _serial(gpu_engine, _roots(53 + trial, 3), RECEIVE)
-        t = time.perf_counter()
-        hits = gpu_engine.sweep(root, 0xffffffc000000000, 0, 1 << 22, device_mask=1)
-        dt = time.perf_counter() - t
-        assert dt < 0.012, f"sweep took {dt * 1e3:.1f} ms behind a lingering launch"
-        assert sorted(hits) == oracle.sweep(root, 0xffffffc000000000, 0, 1 << 22)
-
-
-def test_values_and_bounded_searches_after_a_search(gpu_engine):
-    root = _roots(54, 1)[0]
-    gpu_engine.values(root, 0, 64, device=0)  # first calls load their kernels
-    gpu_engine.submit(root, (1 << 64) - 1, start=0, device_mask=1, max_nonces_per_device=1 << 20).wait(30)
-    for trial in range(3):
-        _serial(gpu_engine, _roots(55 + trial, 3), RECEIVE)
-        t = time.perf_counter()
-        vals = gpu_engine.values(root, 1000, 4096, device=0)
-        assert time.perf_counter() - t < 0.012
-        assert vals == oracle.work_values([root] * 4096, [1000 + i for i in range(4096)])
-        _serial(gpu_engine, _roots(58 + trial, 2), RECEIVE)
-        t = time.perf_counter()
-        res = gpu_engine.submit(root, (1 << 64) - 1, start=5 << 30, device_mask=1,
-                                max_nonces_per_device=1 << 24).wait(30)
-        dt = time.perf_counter() - t
-        assert res.status == _lib.NPOW_EXHAUSTED and res.nonces_done == 1 << 24
-        assert dt < 0.015, f"bounded search took {dt * 1e3:.1f} ms behind a lingering launch"
-
-
-def test_an_idle_lingering_launch_ends(gpu_engine):
-    """Idle past its time budget, the lingering launch ends (the worker raises end_linger, the kernel gives up after
-    a budget's worth of waiting anyway): the next search starts a launch of its own instead of joining it."""
-    _serial(gpu_engine, _roots(61, 2), RECEIVE)
-    time.sleep(0.08)  # > the 20-ms budget
-    assert gpu_engine.pool_status() == (0, 0)
-    before = gpu_engine.stats(0)
-    _serial(gpu_engine, _roots(62, 1), RECEIVE)
-    after = gpu_engine.stats(0)
-    assert after.launches == before.launches + 1 and after.dyn_entries == before.dyn_entries
+def totals():
+    st = [eng.stats(d) for d in range(G)]
+    return {"devices": G, "launches": sum(s.launches for s in st), "dyn": sum(s.dyn_entries for s in st),
+            "nonces": sum(s.nonces for s in st), "mismatch": sum(s.early_mismatches for s in st)}
+"""
 
 
 def _child(env_extra, code):
     env = dict(os.environ, **env_extra)
-    p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=110,
+    for k in [k for k, v in env_extra.items() if v is None]:
+        env.pop(k)
+    p = subprocess.run([sys.executable, "-c", PRELUDE + code], env=env, capture_output=True, text=True, timeout=110,
                        cwd=ROOT)
     assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
     return json.loads(p.stdout.strip().splitlines()[-1])
 
 
-CHILD = r"""
-import json, random, sys
-sys.path.insert(0, "nano-dpow_amd"); sys.path.insert(0, "oracle")
-import nanopow, oracle
-eng = nanopow.engine()
-G = eng.n_devices
-mask = (1 << G) - 1
-rng = random.Random(71)
-roots = [bytes(rng.getrandbits(8) for _ in range(32)) for _ in range(120)]
+def _serial(n):
+    return r"""
 for d in range(G):
     eng.reset_stats(d)
-done = 0
-for i, r in enumerate(roots):
-    res = eng.submit(r, 0xfffffe0000000000, start=i << 40, device_mask=mask).wait(30)
-    assert res.status == 0 and oracle.work_value_hashlib(r, res.nonce) == res.value >= 0xfffffe0000000000, i
-    done += res.nonces_done
-st = [eng.stats(d) for d in range(G)]
-print(json.dumps({"devices": G, "launches": sum(s.launches for s in st), "dyn": sum(s.dyn_entries for s in st),
-                  "nonces": sum(s.nonces for s in st), "done": done,
-                  "mismatch": sum(s.early_mismatches for s in st)}))
-"""
+done = serial(roots(51, %d))
+out = totals(); out["done"] = done
+print(json.dumps(out))
+""" % n
+
+
+def test_serial_searches_join_the_lingering_launch():
+    out = _child({"NANOPOW_LINGER": "1"}, _serial(300))
+    # ~0.2 ms per search: a 20-ms launch serves its table entry and up to 32 dynamic entries
+    assert out["launches"] < 300 // 4 and out["dyn"] >= 300 // 2, out
+    assert out["nonces"] == out["done"] and out["mismatch"] == 0, out
+
+
+def test_one_device_does_not_linger_by_default():
+    out = _child({"NANOPOW_LINGER": None, "NANOPOW_VIRTUAL_DEVICES": None}, _serial(100))
+    assert out["devices"] == 1 and out["dyn"] == 0 and out["launches"] >= 100, out
+    assert out["nonces"] == out["done"] and out["mismatch"] == 0, out
+
+
+def test_cu_partitions_linger_by_default():
+    out = _child({"NANOPOW_LINGER": None, "NANOPOW_VIRTUAL_DEVICES": "4"}, _serial(120))
+    assert out["devices"] == 4
+    assert out["launches"] < 4 * 120 // 4 and out["dyn"] >= 4 * 120 // 2, out
+    assert out["nonces"] == out["done"] and out["mismatch"] == 0, out
 
 
 def test_linger_off_gives_one_launch_per_search():
-    out = _child({"NANOPOW_LINGER": "0"}, CHILD)
-    assert out["dyn"] == 0 and out["launches"] >= 120
-    assert out["nonces"] == out["done"] and out["mismatch"] == 0
-
-
-def test_split_searches_linger_on_cu_partitions():
-    out = _child({"NANOPOW_VIRTUAL_DEVICES": "4"}, CHILD)
-    assert out["devices"] == 4
-    assert out["launches"] < 4 * 120 // 4 and out["dyn"] >= 4 * 120 // 2, out
+    out = _child({"NANOPOW_VIRTUAL_DEVICES": "4", "NANOPOW_LINGER": "0"}, _serial(120))
+    assert out["dyn"] == 0 and out["launches"] >= 4 * 120
     assert out["nonces"] == out["done"] and out["mismatch"] == 0
 
 
 def test_time_shared_devices_do_not_linger():
     """Logical devices time-sharing the whole GPU (NANOPOW_VIRTUAL_PARTITION=share): a lingering launch's sleeping
     waves would hold the CUs from the other devices' launches, so none lingers."""
-    out = _child({"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_VIRTUAL_PARTITION": "share"}, CHILD)
+    out = _child({"NANOPOW_VIRTUAL_DEVICES": "2", "NANOPOW_VIRTUAL_PARTITION": "share", "NANOPOW_LINGER": "1"},
+                 _serial(120))
     assert out["devices"] == 2 and out["dyn"] == 0
     assert out["nonces"] == out["done"] and out["mismatch"] == 0
+
+
+TASKS = r"""
+root = roots(52, 1)[0]
+eng.sweep(root, 0xffffffc000000000, 0, 1 << 22, device_mask=1)  # first calls load their kernels (~20 ms)
+eng.values(root, 0, 64, device=0)
+eng.submit(root, (1 << 64) - 1, start=0, device_mask=1, max_nonces_per_device=1 << 20).wait(30)
+times = {"sweep": [], "values": [], "bounded": []}
+for trial in range(3):
+    serial(roots(53 + trial, 3), mask=1)
+    t = time.perf_counter()
+    hits = eng.sweep(root, 0xffffffc000000000, 0, 1 << 22, device_mask=1)
+    times["sweep"].append(time.perf_counter() - t)
+    assert sorted(hits) == oracle.sweep(root, 0xffffffc000000000, 0, 1 << 22)
+    serial(roots(56 + trial, 3), mask=1)
+    t = time.perf_counter()
+    vals = eng.values(root, 1000, 4096, device=0)
+    times["values"].append(time.perf_counter() - t)
+    assert vals == oracle.work_values([root] * 4096, [1000 + i for i in range(4096)])
+    serial(roots(59 + trial, 3), mask=1)
+    t = time.perf_counter()
+    res = eng.submit(root, (1 << 64) - 1, start=5 << 30, device_mask=1, max_nonces_per_device=1 << 24).wait(30)
+    times["bounded"].append(time.perf_counter() - t)
+    assert res.status == _lib.NPOW_EXHAUSTED and res.nonces_done == 1 << 24
+# an idle lingering launch ends (the worker's 1-ms wait, the kernel's own limit): the next search gets a launch
+serial(roots(62, 2), mask=1)
+time.sleep(0.08)
+before = eng.stats(0)
+serial(roots(63, 1), mask=1)
+after = eng.stats(0)
+print(json.dumps({"times": times, "idle_new_launch": after.launches - before.launches,
+                  "idle_new_dyn": after.dyn_entries - before.dyn_entries, "pool": list(eng.pool_status())}))
+"""
+
+
+def test_tasks_and_bounded_searches_do_not_wait_for_a_lingering_launch():
+    out = _child({"NANOPOW_LINGER": "1"}, TASKS)
+    assert max(out["times"]["sweep"]) < 0.012 and max(out["times"]["values"]) < 0.012, out
+    assert max(out["times"]["bounded"]) < 0.015, out
+    assert out["idle_new_launch"] == 1 and out["idle_new_dyn"] == 0, out
+    assert out["pool"] == [0, 0]
