@@ -85,16 +85,23 @@ const bool g_debug = getenv("NANOPOW_DEBUG") != nullptr;
 // Lingering launches (round 5, PoolTable::linger): an unbounded launch's workgroups wait in it for the next dynamic
 // entry once its entries are over, so a serial client's next search joins the running launch instead of needing one.
 // The worker ends a launch that has lingered g_linger_us with nothing to do (end_linger): its sleeping waves hold the
-// CUs, and a serial client's next search comes within ~0.1 ms.  Measured: over 8 CU partitions
-// the 2^26-nonce regime's node rate 0.95 -> 0.985-0.99 of the devices' full rate, on one device no gain (0.99-1.0
-// either way, the bench -0.1 to -0.3 %: each workgroup's acquire of a new entry spreads their start).  So by default
-// on when the pool has 2 or more GPU devices (pool_start); NANOPOW_LINGER=1 / 0 forces it on / off, NANOPOW_LINGER_US
-// sets the wait.  Never for logical devices that time-share a GPU (Device::time_shared).
+// CUs, and a serial client's next search comes within ~0.1 ms.  Measured on the 2^26-nonce regime, interleaved with
+// the same roots (profiles/r05aj_linger_by_partition_regime_ab.jsonl): over 8 CU partitions of 32
+// CUs the node rate goes 0.956 -> 0.98-0.99 of the devices' full rate with the p50 within +-0.05 ms; over 4, 2 and 1
+// (64 CUs and more) it costs -- node rate 0.97-0.995 against 0.996-1.0, p50 0.04-0.19 ms later -- since each
+// workgroup's acquire of a new entry (an L2 invalidation each) spreads their start, the more the more workgroups share
+// an XCD.  So by default on only for CU partitions of at most kLingerMaxCus CUs (lingers(); a whole GPU, and so every
+// physical GPU of a node, launches per search); NANOPOW_LINGER=1 / 0 forces it on / off, NANOPOW_LINGER_US sets the
+// wait.  Never for logical devices that time-share a GPU (Device::time_shared).
 const int g_linger_env = [] {
   const char* e = getenv("NANOPOW_LINGER");
   return e ? (e[0] == '0' ? 0 : 1) : -1;
 }();
-bool g_linger = false;  // pool_start
+constexpr int kLingerMaxCus = 32;
+static bool lingers(const Device& d) {
+  if (d.time_shared) return false;
+  return g_linger_env >= 0 ? g_linger_env == 1 : (d.cu_first >= 0 && d.cus <= kLingerMaxCus);
+}
 const uint32_t g_linger_p = [] {  // NANOPOW_LINGER_P (A/B runs): the pinned-read period in looks (a power of two)
   const char* e = getenv("NANOPOW_LINGER_P");
   uint32_t p = e ? (uint32_t)atoi(e) : 0u, q = 1;
@@ -1078,7 +1085,7 @@ int Worker::launch(bool empty_linger) {
       sl.fresh = false;
     }
   }
-  if (g_linger && !d_.time_shared && !bounded && g_budget_us.load() > 0) {
+  if (lingers(d_) && !bounded && g_budget_us.load() > 0) {
     // each lingering workgroup reads the pinned ctl word once in P looks (phase g): ~2 reads per look grid-wide
     uint32_t P = 1;
     while (P * 2 < (uint32_t)sh.grid) P <<= 1;
@@ -1521,9 +1528,6 @@ void pool_start() {
     g_pool.running = true;
     g_pool.stopping = false;
   }
-  int gpus = 0;
-  for (auto& d : g_devs) gpus += d->cpu_threads == 0 ? 1 : 0;
-  g_linger = g_linger_env >= 0 ? g_linger_env == 1 : gpus >= 2;
   if (g_watcher_on) {
     {
       std::lock_guard<std::mutex> g(g_watch.mu);
