@@ -7,6 +7,7 @@ unknown action and read ['error'] (:53); serial work_generate and read ['work']
 which must then answer {"error": "Cancelled"} (:61-80, :109-114).
 """
 import json
+import socket
 import threading
 import time
 import urllib.request
@@ -247,21 +248,35 @@ def test_concurrent_requests_share_the_pool():
 
 def test_burst_of_concurrent_connections_is_accepted_at_once():
     """300 clients connect at the same moment (a precache wave from many DPoW clients): the
-    listener's backlog holds them all, so no request waits out TCP's 1-s SYN retry."""
+    listener's backlog holds them all, so no connection waits out TCP's 1-s SYN retry.  Timed is
+    the connect itself: the whole request's time under 600 Python threads on a loaded CI host
+    reaches ~1 s by CPU contention alone, which is not what the backlog is about."""
     eng = OracleEngine(chunk=1 << 12, delay=0.0)
     srv = HttpWorkServer(WorkServer(eng, max_active=64), "127.0.0.1", 0).start()
+    host, port = srv.address.split(":")
     n = 300
-    lat, out = [0.0] * n, [None] * n
+    conn_s, out = [0.0] * n, [None] * n
     go = threading.Event()
 
     def client(i):
         go.wait()
         t = time.perf_counter()
-        # a trivial difficulty (~1 nonce per request): the latency measured is the connection's,
-        # not the oracle engine's CPU hashing under 300 threads
-        out[i] = post(srv.address, {"action": "work_generate", "hash": f"{i + 1:064X}", "difficulty": "1000000000000000"},
-                      timeout=60)
-        lat[i] = time.perf_counter() - t
+        with socket.create_connection((host, int(port)), timeout=60) as s:
+            conn_s[i] = time.perf_counter() - t
+            # a trivial difficulty (~1 nonce per request): the oracle engine's CPU hashing stays out of it
+            body = json.dumps({"action": "work_generate", "hash": f"{i + 1:064X}",
+                               "difficulty": "1000000000000000"}).encode()
+            s.sendall(b"POST / HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\nConnection: close\r\n"
+                      b"Content-Length: %d\r\n\r\n" % len(body) + body)
+            buf = b""
+            while True:
+                d = s.recv(65536)
+                if not d:
+                    break
+                buf += d
+        head, _, payload = buf.partition(b"\r\n\r\n")
+        assert head.startswith(b"HTTP/1.1 200"), head
+        out[i] = json.loads(payload)
     try:
         ths = [threading.Thread(target=client, args=(i,)) for i in range(n)]
         for t in ths:
@@ -273,9 +288,8 @@ def test_burst_of_concurrent_connections_is_accepted_at_once():
         srv.stop()
     for i in range(n):
         assert oracle.work_value(bytes.fromhex(f"{i + 1:064X}"), int(out[i]["work"], 16)) >= 0x1000000000000000
-    # a listen backlog overflow would send dozens of them through TCP's 1-s SYN retry; allow a
-    # few stragglers to a loaded CI host
-    assert sum(1 for x in lat if x >= 0.9) <= 10, sorted(lat)[-12:]
+    # a listen backlog overflow would send dozens of them through TCP's 1-s SYN retry
+    assert sum(1 for x in conn_s if x >= 0.9) <= 2, sorted(conn_s)[-12:]
 
 
 def test_reference_workhandler_against_this_server():
