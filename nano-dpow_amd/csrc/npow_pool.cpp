@@ -1330,13 +1330,22 @@ int Worker::step() {
   if (!q_.empty() && !live_slot()) {
     // a lingering launch idle for g_linger_us, or something waiting for the device, or its time budget over.  Idle
     // means also no won or killed slot still draining in it (its final count not in): ended under such a slot, the
-    // launch's yield would race the kill relay (npow_kernel.hip ls2_poll)
-    bool draining = false;
-    for (const Slot& sl : slots_)
-      draining = draining || (sl.state == SlotState::kDraining && !sl.fin_seen && !sl.inflight.empty());
+    // launch's yield would race the kill relay (npow_kernel.hip ls2_poll).  A slot whose final count has not come
+    // g_linger_us after its stop no longer holds the launch (stale): its count then comes from the launch's completion
+    // and the read-back -- rare (1 search in ~1,200 over 4 CU partitions, profiles/r05aj_linger_by_partition_overshoot
+    // .jsonl), but without this bound the lingering launch ran on to its budget and the stop took 21 ms.
     const double t = now_us();
+    bool draining = false, stale = false;
+    for (const Slot& sl : slots_) {
+      if (sl.state != SlotState::kDraining || sl.fin_seen || sl.inflight.empty()) continue;
+      if (sl.stop_us > 0 && t - sl.stop_us > g_linger_us)
+        stale = true;
+      else
+        draining = true;
+    }
     if (idle_since_ == 0 && !draining) idle_since_ = t;
     bool waiting = d_.tasks_waiting.load() > 0 || d_.dead || g_pool.stopping.load(std::memory_order_relaxed) ||
+                   (stale && !draining) ||
                    (idle_since_ > 0 && t - idle_since_ > g_linger_us) ||
                    std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - front_start_).count() >
                        (double)g_budget_us.load();
