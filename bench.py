@@ -1105,19 +1105,44 @@ def _hashlib_search(root: bytes, thr: int, start: int, limit: int):
 
 class KeepAliveClient:
     """One persistent HTTP/1.1 connection to the work server, as the DPoW client's aiohttp session
-    keeps one for its serial work_generate loop (client/work_handler.py:98-108)."""
+    keeps one for its serial work_generate loop (client/work_handler.py:98-108).  A lean client: one
+    send per request (TCP_NODELAY), the reply read by its Content-Length -- aiohttp parses with a C
+    parser, while http.client's Python header parsing added ~0.3 ms per request on this container and
+    stood in the measured HTTP hop (round 5, tools/experiments/http_hop.py)."""
 
     def __init__(self, address: str):
-        import http.client
+        import socket
         host, port = address.rsplit(":", 1)
-        self.conn = http.client.HTTPConnection(host, int(port), timeout=120)
+        self.sock = socket.create_connection((host, int(port)), timeout=120)
+        self.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        self.buf = b""
 
     def post(self, obj):
-        self.conn.request("POST", "/", json.dumps(obj), {"Content-Type": "application/json"})
-        return json.loads(self.conn.getresponse().read())
+        body = json.dumps(obj).encode()
+        self.sock.sendall(b"POST / HTTP/1.1\r\nHost: localhost\r\nContent-Type: application/json\r\n"
+                          b"Content-Length: %d\r\n\r\n" % len(body) + body)
+        while b"\r\n\r\n" not in self.buf:
+            self._recv()
+        head, _, rest = self.buf.partition(b"\r\n\r\n")
+        lines = head.split(b"\r\n")
+        if not lines[0].startswith(b"HTTP/1.1 200"):
+            raise RuntimeError(f"HTTP reply {lines[0]!r}")
+        n = next(int(v) for k, _, v in (h.partition(b":") for h in lines[1:]) if k.strip().lower() == b"content-length")
+        while len(rest) < n:
+            self.buf = rest
+            self._recv()
+            rest = self.buf
+        self.buf = rest[n:]
+        return json.loads(rest[:n])
+
+    def _recv(self):
+        d = self.sock.recv(65536)
+        if not d:
+            raise RuntimeError("the work server closed the connection")
+        self.buf += d
 
     def close(self):
-        self.conn.close()
+        self.sock.close()
 
 
 def _http_ttw(eng, n, thr=SEND, base=30_000_000, device_mask=1):
@@ -1550,12 +1575,11 @@ def regime_child(n_dev: int, m: int, timeout: float = 150.0):
 
 
 def workload_receive(eng, args, rank, world, dist):
-    """BASELINE config 1: work_generate at fffffe0000000000, GPU next to the CPU reference."""
+    """BASELINE configs[0]: work_generate at fffffe0000000000, GPU next to the CPU reference."""
     if world > 1:
         raise SystemExit("--workload receive runs in one process")
     recv = 0xfffffe0000000000
     from nanopow.server import HttpWorkServer, WorkServer
-    import urllib.request
     # GPU through the C ABI
     gpu = []
     for i in range(args.steps):
@@ -1572,9 +1596,11 @@ def workload_receive(eng, args, rank, world, dist):
             body = json.dumps({"action": "work_generate", "hash": bench_root(23_000_000 + i).hex(),
                                "difficulty": f"{recv:016x}"}).encode()
             t = time.perf_counter()
-            req = urllib.request.Request(f"http://{srv.address}", data=body, method="POST")
-            with urllib.request.urlopen(req, timeout=60) as resp:
-                rep = json.loads(resp.read())
+            cli = KeepAliveClient(srv.address)  # a new connection for this request alone
+            try:
+                rep = cli.post(json.loads(body))
+            finally:
+                cli.close()
             http_new.append(time.perf_counter() - t)
             assert "work" in rep
     finally:
