@@ -425,14 +425,60 @@ class _Connection(socketserver.StreamRequestHandler):
             pass  # the client went away; its request was answered as far as the server is concerned
 
 
-class _Listener(socketserver.ThreadingTCPServer):
+class _Listener(socketserver.TCPServer):
+    """Accepts connections and hands each to a connection thread (one per open connection: a DPoW
+    client's keep-alive session holds its thread).  Threads that finish a connection wait for the
+    next one (up to _MAX_IDLE of them) instead of exiting: a request on a new connection then costs
+    a queue hand-off, not a thread start (round 5: ~0.3 ms per request on the MI355X box's host with
+    a thread per connection, profiles/r05as_http_new_connection.json)."""
     # socketserver's default listen backlog is 5: a burst of concurrent work_generate
     # connections (many clients, or one client's precache wave) would overflow it and wait
     # out TCP's 1-s SYN retry, or be reset.  4,096 connections at once (BASELINE configs[3])
     # overflowed 1,024 with resets; the kernel caps this at net.core.somaxconn.
     request_queue_size = 8192
     allow_reuse_address = True
-    daemon_threads = True
+    _MAX_IDLE = 64
+
+    def __init__(self, address, handler) -> None:
+        super().__init__(address, handler)
+        self._conns: "queue.SimpleQueue" = queue.SimpleQueue()
+        self._pool_lock = threading.Lock()
+        self._idle = 0       # connection threads waiting for a connection, not yet promised one
+        self._closed = False
+
+    def process_request(self, request, client_address) -> None:
+        with self._pool_lock:
+            spawn = self._idle == 0
+            if not spawn:
+                self._idle -= 1  # that thread takes this connection
+        self._conns.put((request, client_address))
+        if spawn:
+            threading.Thread(target=self._connection_thread, name="nanopow-conn", daemon=True).start()
+
+    def _connection_thread(self) -> None:
+        while True:
+            item = self._conns.get()
+            if item is None:
+                return
+            request, client_address = item
+            try:
+                self.finish_request(request, client_address)
+            except Exception:
+                self.handle_error(request, client_address)
+            finally:
+                self.shutdown_request(request)
+            with self._pool_lock:
+                if self._closed or self._idle >= self._MAX_IDLE:
+                    return
+                self._idle += 1
+
+    def server_close(self) -> None:
+        super().server_close()
+        with self._pool_lock:
+            self._closed = True
+            idle, self._idle = self._idle, 0
+        for _ in range(idle):
+            self._conns.put(None)
 
 
 class HttpWorkServer:
