@@ -228,3 +228,6 @@ def test_regime_harness_with_oracle_engine():
     bad = bench.device_check([4.3, 4.31, 3.5], 1000, 1000)
     assert not bad["ok"] and bad["slow_devices"] == [2]
     assert not bench.device_check([4.3, 4.3], 999, 1000)["ok"]  # counters that do not sum
+    # per MHz when the clocks are known: a GPU at a lower power-capped clock is no fault, a slow one at its clock is
+    assert bench.device_check([35.0, 32.4], 10, 10, [2340.0, 2170.0])["ok"]
+    assert bench.device_check([35.0, 35.0, 31.0], 10, 10, [2340.0] * 3)["slow_devices"] == [2]
