@@ -368,9 +368,12 @@ extern "C" {
 
 const char* npow_last_error(void) { return t_err.c_str(); }
 
+#define NPOW_STR2(x) #x
+#define NPOW_STR(x) NPOW_STR2(x)
 const char* npow_version(void) {
-  return "libnanopow 0.4 (ABI 4; gfx950 HIP kernels: blake2b-64 nonce search, four 512-lane workgroups per CU, priority runs; "
-         "v_lshl_add_u64 adds, v_alignbit rotations)";
+  // the ABI number from the header itself: the round-5 string still said "ABI 4" after the header moved to 5
+  return "libnanopow 0.5 (ABI " NPOW_STR(NPOW_ABI_VERSION) "; gfx950 HIP kernels: blake2b-64 nonce search, four "
+         "512-lane workgroups per CU, priority runs; v_lshl_add_u64 adds, v_alignbit rotations)";
 }
 
 int npow_abi_version(void) { return NPOW_ABI_VERSION; }
