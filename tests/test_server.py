@@ -426,3 +426,23 @@ def test_connection_threads_are_reused(server, monkeypatch):
                 buf += d
         assert buf.startswith(b"HTTP/1.1 200") and b"valid_all" in buf
     assert 1 <= len(served) <= 3, len(served)
+
+
+def test_bench_keepalive_client_against_the_server(server):
+    """bench.py's lean keep-alive client (the HTTP legs of the bench) against this server: several requests
+    on one connection, each reply parsed by its Content-Length and re-validated."""
+    import sys
+    from conftest import ROOT
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+    srv, _eng = server
+    cli = bench.KeepAliveClient(srv.address)
+    try:
+        for i in range(5):
+            root = f"{i + 7:064X}"
+            rep = cli.post({"action": "work_generate", "hash": root, "difficulty": "ff00000000000000"})
+            assert oracle.work_value(bytes.fromhex(root), int(rep["work"], 16)) >= 0xff00000000000000
+        assert "valid_all" in cli.post({"action": "work_validate", "hash": "00" * 32, "work": "0" * 16})
+    finally:
+        cli.close()
