@@ -61,8 +61,10 @@ extern "C" {
  * 5: npow_search_info gains the search's host timeline (adopt_us, launch_us, launch_all_us, win_seen_us);
  * npow_device_stats gains idle_ms / idle_gaps (the GPU idle between the device's search launches) and
  * affinity_checks / affinity_failures (NANOPOW_TEST_HOOKS=1, since npow_init: the calling thread's HIP device checked
- * at every HIP call site of the device) and watcher_decisions.  Both structs are still written up to the size the caller passes. */
-#define NPOW_ABI_VERSION 5
+ * at every HIP call site of the device) and watcher_decisions.  Both structs are still written up to the size the caller passes.
+ * 6: npow_device_stats gains stale_drains (a protocol check: won or killed jobs of a lingering launch whose final count
+ * never came) and linger_ms (the device's lingering launches waiting with nothing to hash, inside kernel_ms). */
+#define NPOW_ABI_VERSION 6
 
 /* Hash paths of npow_values_path. */
 #define NPOW_PATH_SEARCH 0  /* the instruction stream the search and sweep kernels execute
@@ -116,6 +118,11 @@ typedef struct npow_device_stats {
   uint64_t affinity_failures; /* ... and found wrong (the call then fails: NPOW_ERR_INTERNAL) */
   uint64_t watcher_decisions; /* jobs decided by the process's win watcher from this device's win records (it spins
                                  over every live slot's record; NANOPOW_WATCHER=0 leaves them to the device's worker) */
+  /* ---- ABI 6 ---- */
+  uint64_t stale_drains;    /* won or killed jobs of a lingering launch whose final count the kernel had not published
+                               1 ms after the stop (the worker then ended the launch and read the count back): 0 */
+  double linger_ms;         /* of kernel_ms, the time this device's lingering launches waited with nothing to hash
+                               (host-timed): (kernel_ms - linger_ms) is the time the device hashed */
 } npow_device_stats;
 
 /* Outcome of one search (npow_wait_info).  Times are host steady-clock microseconds since

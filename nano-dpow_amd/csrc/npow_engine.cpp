@@ -372,7 +372,7 @@ const char* npow_last_error(void) { return t_err.c_str(); }
 #define NPOW_STR(x) NPOW_STR2(x)
 const char* npow_version(void) {
   // the ABI number from the header itself: the round-5 string still said "ABI 4" after the header moved to 5
-  return "libnanopow 0.5 (ABI " NPOW_STR(NPOW_ABI_VERSION) "; gfx950 HIP kernels: blake2b-64 nonce search, four "
+  return "libnanopow 0.6 (ABI " NPOW_STR(NPOW_ABI_VERSION) "; gfx950 HIP kernels: blake2b-64 nonce search, four "
          "512-lane workgroups per CU, priority runs; v_lshl_add_u64 adds, v_alignbit rotations)";
 }
 
@@ -569,6 +569,8 @@ static int stats_fill(int device, npow_device_stats* out) {
   out->affinity_checks = d.affinity_checks.load(std::memory_order_relaxed);
   out->affinity_failures = d.affinity_failures.load(std::memory_order_relaxed);
   out->watcher_decisions = d.watcher_decisions;
+  out->stale_drains = d.stale_drains;
+  out->linger_ms = d.linger_ms;
   return NPOW_OK;
 }
 
@@ -597,8 +599,8 @@ int npow_device_stats_reset(int device) try {
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
   d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = d.kills_relayed = d.late = 0;
-  d.idle_gaps = d.watcher_decisions = 0;
-  d.idle_ms = 0.0;
+  d.idle_gaps = d.watcher_decisions = d.stale_drains = 0;
+  d.idle_ms = d.linger_ms = 0.0;
   d.kernel_ms = 0.0;
   d.clk_ticks = d.clk_ref_ticks = 0.0;
   d.stats_t0 = std::chrono::steady_clock::now();

@@ -68,6 +68,8 @@ struct Device {
   uint64_t kills_relayed = 0;              // losing jobs stopped by another device's decision (npow_pool.cpp)
   uint64_t late = 0;                       // device-side overshoot: nonces hashed after the job was known over
   uint64_t watcher_decisions = 0;          // jobs the win watcher decided from this device's win records
+  uint64_t stale_drains = 0;               // won / killed slots of a lingering launch whose final count never came
+  double linger_ms = 0.0;                  // host-timed waits of lingering launches with nothing to hash (in kernel_ms)
   double idle_ms = 0.0;                    // GPU idle between consecutive search launches (HIP events) ...
   uint64_t idle_gaps = 0;                  // ... over this many pairs (npow_pool.cpp Worker::retire)
   // Published by the pool worker for npow_device_stats_get: it has launches or slots in flight, and

@@ -758,6 +758,32 @@ __device__ __forceinline__ uint32_t ls2_choose(const PoolTable* tab, PoolDevStat
 // The pinned word is read by ~2 lingering workgroups per look period grid-wide (phase (k + g) mod P, P ~ G / 2), each
 // of which raises PoolDevState::ctl_mirror to it; the others look at the mirror in device memory.  Between looks the
 // wave sleeps ~1.8 us (s_sleep 64: 64 x 64 clocks); the other waves of the workgroup wait at the barrier after it.
+// Round 6: lingering waves poll no kill word, so an entry whose hashing workgroups had all left it
+// while it was live -- the launch's time budget ends a hashing workgroup (kind 0) while others linger on, up to a
+// budget past their own entry into ls2_linger -- had nobody to relay its kill: its final count was not published until
+// the host gave up on it (1 ms) and ended the launch, and until then nobody hashed it either.  Now the lingering
+// workgroup that reads the pinned words (about two per look grid-wide) also relays every kill raised since the
+// launch's last relay (the same scan, keyed by (seq, kills), as ls2_poll's: a dead entry with no workgroup on it is
+// published at once by ls2_kill) and looks at all of the launch's live entries again, not only new ones (such an entry
+// is joined and hashed again; past the launch's budget its joiners leave within 4 iterations, ending the launch).
+// Lane 0.  (Inlined: the search loop keeps its register allocation, tools/kernel_loop_census.py, and no call frame.)
+__device__ __forceinline__ void ls2_linger_relay(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t nd) {
+  const uint32_t kills = (uint32_t)__hip_atomic_load(&mb->kills, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  unsigned long long* const kd = &st->kills_done[tab->ring & (kPoolRing - 1)][0];
+  const unsigned long long key = ((unsigned long long)tab->seq << 32) | kills;
+  if (kills == tab->kill_base || __hip_atomic_load(kd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == key) return;
+  __atomic_signal_fence(__ATOMIC_SEQ_CST);  // the kill words after the counter (ls2_poll)
+  const unsigned long long over = __hip_atomic_load(&s_over, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  for (uint32_t k = 0; k < tab->n + nd; ++k) {
+    if ((over >> k) & 1) continue;
+    const EntryHdr q = ls2_hdr(tab, mb, k);
+    if (load_dead(st, q.slot) < q.gen &&
+        __hip_atomic_load(&mb->kill[q.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q.gen)
+      ls2_kill(st, mb, q.slot, q.gen, true);  // (a lingering launch is counted)
+  }
+  __hip_atomic_store(kd, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ uint32_t ls2_linger(const PoolTable* tab, PoolDevState* st, PoolMailbox* mb, uint32_t* seen,
                                             uint32_t looked) {
   const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
@@ -769,7 +795,8 @@ __device__ __forceinline__ uint32_t ls2_linger(const PoolTable* tab, PoolDevStat
   for (uint32_t k = 0;; ++k) {
     if ((uint32_t)__builtin_amdgcn_s_memrealtime() - t_enter >= tab->budget) return kNoEntry;
     uint64_t ctl;
-    if (((k + g) & (P - 1)) == 0) {
+    const bool pinned = ((k + g) & (P - 1)) == 0;
+    if (pinned) {
       ctl = ls2_ctl(mb);
       __hip_atomic_fetch_max(mirror, (unsigned long long)ctl, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
@@ -779,7 +806,11 @@ __device__ __forceinline__ uint32_t ls2_linger(const PoolTable* tab, PoolDevStat
     if ((int32_t)(hi - base_hi) > 0) return kNoEntry;  // a yield since the table was built
     if (hi == base_hi) {                               // (an older mirror value: no news)
       const uint32_t nd = ls2_dyn_count_since(tab, ctl);
-      if (nd > looked) {
+      if (pinned) {
+        if (lane == 0) ls2_linger_relay(tab, st, mb, nd);
+        looked = 0;  // every live entry again (above)
+      }
+      if (nd > looked || (pinned && tab->n > 0)) {
         const uint32_t p = ls2_choose(tab, st, mb, kNoEntry, nd, seen, lane, g);
         if (p != kNoEntry) return p;
         looked = nd;  // (joined by others and over already, or cancelled)

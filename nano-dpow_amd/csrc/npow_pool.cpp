@@ -195,15 +195,34 @@ double now_us() {
 }
 Pool g_pool;
 std::atomic<uint64_t> g_gen{0};
-std::atomic<bool> g_exiting{false};  // process exit: workers leave at once, no further HIP calls
+std::atomic<bool> g_exiting{false};
+std::atomic<double> g_exit_deadline_us{0.0};
 
-// -- job state transitions (caller holds g_pool.mu) ------------------------------------------
-static void notify_waiters(Job& j) {
+bool exit_now() {
+  if (g_exiting.load(std::memory_order_relaxed)) return true;
+  const double d = g_exit_deadline_us.load(std::memory_order_relaxed);
+  if (d > 0 && now_us() > d) {
+    g_exiting.store(true);
+    return true;
+  }
+  return false;
+}
+
+// -- deferred notifications (PoolLock, npow_pool.h) ----------------------------------------------
+namespace {
+struct Deferred {
+  int depth = 0;
+  bool workers = false;
+  std::vector<Job*> jobs;
+};
+thread_local Deferred t_defer;
+
+void notify_waiters_now(Job& j) {
   { std::lock_guard<std::mutex> g(j.wmu); }  // a waiter between its check and its wait cannot miss the notify
   j.cv.notify_all();
 }
 
-void notify_workers_locked() {
+void notify_workers_now() {
   g_pool.cv_work.notify_all();
   for (auto& dp : g_devs) {
     Device& d = *dp;
@@ -213,6 +232,38 @@ void notify_workers_locked() {
     }
     d.wake_cv.notify_one();
   }
+}
+}  // namespace
+
+PoolLock::PoolLock() : lk_(g_pool.mu) { t_defer.depth++; }
+
+PoolLock::~PoolLock() {
+  lk_.unlock();
+  if (--t_defer.depth > 0) return;
+  // the states these wake-ups announce were all written under the lock: a thread woken now finds them
+  std::vector<Job*> jobs;
+  jobs.swap(t_defer.jobs);
+  const bool workers = t_defer.workers;
+  t_defer.workers = false;
+  for (Job* j : jobs) notify_waiters_now(*j);
+  if (workers) notify_workers_now();
+}
+
+// -- job state transitions (caller holds g_pool.mu) ------------------------------------------
+static void notify_waiters(Job& j) {
+  if (t_defer.depth > 0) {
+    if (std::find(t_defer.jobs.begin(), t_defer.jobs.end(), &j) == t_defer.jobs.end()) t_defer.jobs.push_back(&j);
+    return;
+  }
+  notify_waiters_now(j);
+}
+
+void notify_workers_locked() {
+  if (t_defer.depth > 0) {
+    t_defer.workers = true;
+    return;
+  }
+  notify_workers_now();
 }
 
 void decide_locked(Job& j, int status, uint64_t nonce, uint64_t value) {
@@ -258,11 +309,11 @@ void finish_locked(const JobP& j) {
 }
 
 // Device k of job j is finished with it (retired, exhausted, or the device failed).
-void device_done_locked(const JobP& j, size_t k) {
+void device_done_locked(const JobP& j, size_t k, double t_seen) {
   if (j->dev_done[k]) return;
   j->dev_done[k] = 1;
   j->on_dev[k] = 0;
-  if (j->seen_dev[k] && j->t_stop[k] == 0) j->t_stop[k] = now_us();
+  if (j->seen_dev[k] && j->t_stop[k] == 0) j->t_stop[k] = t_seen > 0 ? t_seen : now_us();
   if (--j->pending_devs == 0) finish_locked(j);
 }
 
@@ -353,11 +404,21 @@ bool wants_device_locked(int dev) {
 // device's invalid streak and the slot's retirement stay its business; a job already decided is left alone).
 // It also watches each armed job's cancel word (a caller's work_cancel, or another rank's first win through a shared
 // word, bench.py node_time_to_work) and wakes the device's worker at once, which then stops the job's waves.
+// Spinning is bounded (round 6): the watcher spins for kWatchSpinUs after a slot was armed or a record
+// changed -- a receive-difficulty search is won well within that -- and then naps g_watch_nap_us at a time (1-us timer
+// slack; an arm wakes it at once), so a long search, or an idle lingering launch, costs a fraction of a core instead
+// of all of it, and a CPU device's hashing threads (--cpu-threads) keep their cores.  NANOPOW_WATCH_NAP_US=0 spins.
 namespace {
+constexpr double kWatchSpinUs = 2000.0;
+const double g_watch_nap_us = [] {
+  const char* e = getenv("NANOPOW_WATCH_NAP_US");
+  return e ? atof(e) : 20.0;
+}();
 struct Watch {
   std::mutex mu;
   std::condition_variable cv;
-  std::atomic<int> armed{0};  // armed slots over all devices
+  std::atomic<int> armed{0};        // armed slots over all devices
+  std::atomic<uint64_t> arms{0};    // arms so far (a new one restarts the spin window)
   bool stop = false;
   std::thread th;
 };
@@ -373,6 +434,8 @@ void watch_arm(Device& d, int s, uint64_t gen, const JobP& j) {
   d.armed_cancel[s].store(j->cancel, std::memory_order_release);
   d.armed_gen[s].store(gen, std::memory_order_release);
   const uint64_t bit = 1ull << s;
+  g_watch.arms.fetch_add(1, std::memory_order_acq_rel);  // (a napping watcher sees it within its nap: no wake-up here,
+                                                         // under the pool lock; a win comes ~0.2 ms after an arm at best)
   if (!(d.armed_mask.fetch_or(bit, std::memory_order_acq_rel) & bit) &&
       g_watch.armed.fetch_add(1, std::memory_order_acq_rel) == 0) {
     { std::lock_guard<std::mutex> g(g_watch.mu); }
@@ -422,7 +485,7 @@ void watch_handle(Device& d, int s, uint64_t gen) {
   if (__atomic_load_n(&pw.gen, __ATOMIC_ACQUIRE) != gen) return;  // the record moved on meanwhile
   if ((faults().invalid_mask >> d.id) & 1) v ^= 1;                 // NANOPOW_FAULT_INVALID (tests)
   if (host_work_value(j->pre.m, n) != v || v < j->threshold) return;  // invalid: the worker's business
-  std::lock_guard<std::mutex> g(g_pool.mu);
+  PoolLock g;  // (j, a local reference, outlives it)
   const int k = index_in(*j, d.id);
   if (j->status != kPending || k < 0 || j->dev_gen[(size_t)k] != gen) return;
   decide_locked(*j, NPOW_OK, n, v);
@@ -441,13 +504,30 @@ void watcher_run() {
   prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
   std::vector<std::vector<uint64_t>> handled(g_devs.size(), std::vector<uint64_t>(kMaxSlots, 0));
   std::vector<std::vector<uint64_t>> cancelled(g_devs.size(), std::vector<uint64_t>(kMaxSlots, 0));
-  for (;;) {
+  uint64_t arms_seen = g_watch.arms.load(std::memory_order_acquire);
+  double t_event = now_us();  // the last arm or record change: spin until kWatchSpinUs after it
+  for (uint32_t round = 0;; ++round) {
     if (g_watch.armed.load(std::memory_order_acquire) == 0) {
       std::unique_lock<std::mutex> lk(g_watch.mu);
       g_watch.cv.wait(lk, [] { return g_watch.stop || g_watch.armed.load(std::memory_order_acquire) > 0; });
       if (g_watch.stop) return;
+      t_event = now_us();
     }
-    if (g_exiting.load(std::memory_order_relaxed)) return;
+    if (exit_now()) return;
+    if ((round & 63u) == 0) {  // (the clock every 64 rounds: a round over a few armed slots is ~0.1 us)
+      const uint64_t a = g_watch.arms.load(std::memory_order_acquire);
+      const double t = now_us();
+      if (a != arms_seen) {
+        arms_seen = a;
+        t_event = t;
+      } else if (g_watch_nap_us > 0 && t - t_event > kWatchSpinUs) {
+        std::unique_lock<std::mutex> lk(g_watch.mu);
+        g_watch.cv.wait_for(lk, std::chrono::duration<double, std::micro>(g_watch_nap_us), [&] {
+          return g_watch.stop || g_watch.arms.load(std::memory_order_acquire) != arms_seen;
+        });
+        if (g_watch.stop) return;
+      }
+    }
     for (size_t di = 0; di < g_devs.size(); ++di) {
       Device& d = *g_devs[di];
       uint64_t m = d.armed_mask.load(std::memory_order_acquire);
@@ -458,6 +538,7 @@ void watcher_run() {
         if (gen && gen != handled[di][s] && __atomic_load_n(&d.pmb->win[s].gen, __ATOMIC_ACQUIRE) == gen) {
           handled[di][s] = gen;
           watch_handle(d, s, gen);
+          t_event = now_us();
         }
         if (gen && gen != cancelled[di][s] && d.armed_cancel[s].load(std::memory_order_acquire)) {
           bool raised;
@@ -501,6 +582,7 @@ struct Slot {
   bool early = false;      // ... and the job was finished from it before retiring
   double stop_us = 0;      // the job was won or killed at this time: the worker polls without napping
                            // until the slot's final count is in (a quick return, and an exact stop time)
+  bool stale = false;      // its final count had not come g_linger_us after stop_us (npow_device_stats.stale_drains)
   struct Issued {
     uint64_t seq, base, count;
   };
@@ -537,6 +619,7 @@ class Worker {
   uint64_t wake_seen_ = 0;  // Device::wake_seq as of this worker's last nap
   uint64_t early_count_ = 0;  // slots finished early so far (every kVerifyEvery-th is still read back)
   double idle_since_ = 0;     // launches in flight but no live slot since (end_linger after g_linger_us), 0 = busy
+  double linger_t_ = 0;       // the last step that found a lingering launch idle (npow_device_stats.linger_ms), 0 = none
   int invalid_streak_ = 0;  // consecutive winners of this device that failed CPU re-validation
   int prev_stop_ring_ = -1;  // ring of the last retired launch (its stop event: the GPU idle before the next one),
                              // -1 when a sweep / values task used the device's events since
@@ -632,6 +715,7 @@ void Worker::adopt() {
     sl.gen = ++g_gen;
     sl.win_seen = sl.requeue = sl.no_more = sl.readback = sl.fin_seen = sl.early = sl.no_readback = false;
     sl.stop_us = 0;
+    sl.stale = false;
     sl.unread = 0;
     sl.fresh = true;
     sl.inflight.clear();
@@ -767,7 +851,7 @@ void Worker::handle_win(int s) {
   uint64_t v = __atomic_load_n(&pw.value, __ATOMIC_RELAXED);
   if ((faults().invalid_mask >> d_.id) & 1) v ^= 1;  // NANOPOW_FAULT_INVALID (tests)
   const uint64_t cpu_v = host_work_value(j.pre.m, n);
-  std::lock_guard<std::mutex> g(g_pool.mu);
+  PoolLock g;  // (the slot holds the job)
   if (j.t_win == 0) j.t_win = t_seen;
   if (cpu_v == v && v >= j.threshold) {
     invalid_streak_ = 0;
@@ -889,12 +973,13 @@ bool Worker::win_published(int s) const {
 // instead of after the launch -- which its other entries may keep running for the rest of its
 // budget.  A yielded entry (the job is re-adopted) or an invalid win (re-armed) waits for retire().
 void Worker::early_finish(int s) {
+  const double t_obs = now_us();  // the device's stop as this worker saw it (not when it got the pool lock)
   Slot& sl = slots_[s];
   sl.fin_seen = true;
   if (win_published(s)) handle_win(s);  // the winner released its record before closing the entry
   const uint64_t total = __atomic_load_n(&d_.pmb->fin[s].total, __ATOMIC_RELAXED);
   const uint64_t late = __atomic_load_n(&d_.pmb->fin[s].late, __ATOMIC_RELAXED);
-  std::lock_guard<std::mutex> g(g_pool.mu);
+  PoolLock g;  // (the slot holds the job)
   Job& j = *sl.job;
   if (g_trace_lat && j.gpu_t_win) {  // GPU timeline (one GPU's clock: CU partitions), from the deciding win
     const double tw = (double)j.gpu_t_win, tr = (double)__atomic_load_n(&d_.pmb->fin[s].t_relay, __ATOMIC_RELAXED);
@@ -937,7 +1022,7 @@ void Worker::early_finish(int s) {
     d_.nonces += delta;
     d_.early++;
   }
-  device_done_locked(sl.job, sl.k);
+  device_done_locked(sl.job, sl.k, t_obs);
 }
 
 void Worker::check_slots() {
@@ -961,7 +1046,7 @@ void Worker::check_slots() {
       watch_stop_cancel(d_, (int)(&sl - slots_));
     } else if (j.decided.load(std::memory_order_relaxed) || j.cancel_seen()) {
       {
-        std::lock_guard<std::mutex> g(g_pool.mu);
+        PoolLock g;  // (the slot holds the job)
         if (!j.decided.load()) {
           j.cancel_req = true;
           decide_locked(j, NPOW_CANCELLED);
@@ -1142,8 +1227,11 @@ int Worker::queue_readbacks() {
           sl.no_readback = true;
           continue;
         }
-      } else if (!sl.fin_seen && sl.stop_us > 0 && !sl.requeue && !sl.inflight.empty()) {
-        continue;  // won or killed: its final count is on the way (or its launches end without one)
+      } else if (!sl.fin_seen && sl.stop_us > 0 && !sl.requeue && !sl.inflight.empty() &&
+                 now_us() - sl.stop_us < g_linger_us) {
+        continue;  // won or killed: its final count is on the way (or its launches end without one) -- for
+                   // g_linger_us at most: then the read-back is queued now, before the next launch is issued
+                   // (ADVICE r05), not behind it; a final count that still comes is checked against it (retire())
       }
     }
     HIPTRY(hipMemcpyAsync(d_.h_done + (size_t)s * row, &d_.pst->done[s][0], row * sizeof(unsigned long long),
@@ -1335,15 +1423,35 @@ int Worker::step() {
     // and the read-back -- rare (1 search in ~1,200 over 4 CU partitions, profiles/r05aj_linger_by_partition_overshoot
     // .jsonl), but without this bound the lingering launch ran on to its budget and the stop took 21 ms.
     const double t = now_us();
-    bool draining = false, stale = false;
-    for (const Slot& sl : slots_) {
+    bool draining = false, stale = false, lingering = false;
+    for (const PoolInflight& f : q_) lingering = lingering || f.linger;
+    for (Slot& sl : slots_) {
       if (sl.state != SlotState::kDraining || sl.fin_seen || sl.inflight.empty()) continue;
-      if (sl.stop_us > 0 && t - sl.stop_us > g_linger_us)
+      if (sl.stop_us > 0 && t - sl.stop_us > g_linger_us) {
         stale = true;
-      else
+        if (!sl.stale && lingering) {  // the fallback below fires for it: counted (tests assert it stays 0)
+          sl.stale = true;
+          std::lock_guard<std::mutex> sg(d_.stats_mu);
+          d_.stale_drains++;
+          NPOW_DBGT("nanopow[%d]: slot %d g%llu: no final count %.0f us after its stop\n", d_.id,
+                    (int)(&sl - slots_), (unsigned long long)sl.gen, t - sl.stop_us);
+        }
+      } else {
         draining = true;
+      }
     }
     if (idle_since_ == 0 && !draining) idle_since_ = t;
+    // the GPU time a lingering launch spends waiting with nothing to hash (its HIP-event time includes it):
+    // npow_device_stats.linger_ms, so that kernel_ms - linger_ms is the time the device hashed
+    if (lingering && !draining && q_.front().linger) {
+      if (linger_t_ > 0) {
+        std::lock_guard<std::mutex> sg(d_.stats_mu);
+        d_.linger_ms += (t - linger_t_) * 1e-3;
+      }
+      linger_t_ = t;
+    } else {
+      linger_t_ = 0;
+    }
     bool waiting = d_.tasks_waiting.load() > 0 || d_.dead || g_pool.stopping.load(std::memory_order_relaxed) ||
                    (stale && !draining) ||
                    (idle_since_ > 0 && t - idle_since_ > g_linger_us) ||
@@ -1363,6 +1471,7 @@ int Worker::step() {
     }
   } else {
     idle_since_ = 0;
+    linger_t_ = 0;
   }
   if (int rc = timed(2, [&] { return queue_readbacks(); })) return rc;  // before the next launch: it no longer holds them
   if (d_.tasks_waiting.load() == 0)                                       // a sweep / values call is waiting: drain instead
@@ -1387,7 +1496,7 @@ void Worker::run() {
     }
   } on_exit{*this};
   for (;;) {
-    if (g_exiting.load(std::memory_order_relaxed)) return;
+    if (exit_now()) return;
     if (d_.dead && !busy()) {
       // a dropped device (drained) hands every job that still names it to that job's survivors
       if (dev_lock_.owns_lock()) dev_lock_.unlock();
@@ -1409,7 +1518,7 @@ void Worker::run() {
       // much as the search itself at receive difficulty.
       const auto spin_end = std::chrono::steady_clock::now() + std::chrono::microseconds(kIdleSpinUs);
       while (g_pool.version.load(std::memory_order_acquire) == seen_version_ &&
-             !g_exiting.load(std::memory_order_relaxed) && d_.tasks_waiting.load() == 0 &&
+             !exit_now() && d_.tasks_waiting.load() == 0 &&
              std::chrono::steady_clock::now() < spin_end)
         cpu_relax();
       if (g_pool.version.load(std::memory_order_acquire) != seen_version_) continue;
@@ -1423,7 +1532,7 @@ void Worker::run() {
       // for it to finish
       prev_stop_ring_ = -1;  // the task records the device's events too
       if (dev_lock_.owns_lock()) dev_lock_.unlock();
-      while (d_.tasks_waiting.load() > 0 && !g_exiting.load(std::memory_order_relaxed))
+      while (d_.tasks_waiting.load() > 0 && !exit_now())
         std::this_thread::sleep_for(std::chrono::microseconds(50));
       continue;
     }
@@ -1557,9 +1666,19 @@ void pool_start() {
   }
 }
 
+// Process exit (npow_init's atexit hook).  Round 6: the workers used to leave at once, without a HIP
+// call, and a lingering launch (up to its 20-ms budget of waiting, polling pinned memory) or a search launch could
+// still be running while the HIP runtime and a profiler's tool library tore down -- the process then died with SIGSEGV
+// in its exit handlers under rocprofv3 (profiles/r05aq_hip_api_trace_overshoot_g4.txt).  Now exit drains like
+// npow_shutdown: every job is cancelled (its kill word raised), lingering launches get their yield, the workers retire
+// their launches and leave once idle -- for up to kExitDrainMs; after that (a device that does not answer) they leave
+// regardless.  The hook runs before the HIP runtime's own exit handlers (it was registered after the runtime was
+// loaded and initialised: atexit runs in reverse order), so the workers' HIP calls (event queries) are still valid.
+constexpr double kExitDrainMs = 250.0;
 void pool_exit() {
-  g_exiting = true;
+  g_exit_deadline_us.store(now_us() + kExitDrainMs * 1e3);
   pool_stop();
+  g_exiting = true;
 }
 
 void pool_stop() {
@@ -1649,7 +1768,7 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
 // condition-variable wake-up (decided -> result in the client p50 11 us).  One core each while
 // they do; NANOPOW_WAIT_SPIN=0 turns it off (A/B runs).
 constexpr int kMaxSpinners = 2;
-constexpr int64_t kSpinUs = 50000;
+constexpr int64_t kSpinUs = 2000;  // (round 6, ADVICE r05: was 50 ms, a whole send-difficulty search of one core each)
 std::atomic<int> g_spinners{0};
 const bool g_wait_spin = [] {
   const char* e = getenv("NANOPOW_WAIT_SPIN");

@@ -86,13 +86,35 @@ struct Pool {
 extern Pool g_pool;  // npow_pool.cpp
 
 extern std::atomic<uint64_t> g_gen;      // slot generations (unique, > 0)
-extern std::atomic<bool> g_exiting;      // process exit: workers leave at once, no further HIP calls
+extern std::atomic<bool> g_exiting;      // process exit, drain over (or its deadline passed): workers leave at once
+// Process exit (pool_exit, round 6): the workers drain their launches like pool_stop until this deadline (steady clock
+// us; 0 = not exiting), then leave.  exit_now(): the deadline has passed (it then sets g_exiting) or g_exiting is set.
+extern std::atomic<double> g_exit_deadline_us;
+bool exit_now();
+
+// The pool lock with its notifications deferred (round 6): the waiters' condition variables and the
+// workers' wakes that decide_locked / finish_locked / stop_other_devices_locked / admit_locked make under it are sent
+// after the lock is released, not while it is held.  Each is a futex wake-up; made under the lock, the woken thread
+// may preempt the holder on its CPU, and every other thread wanting the lock (the losing devices' workers publishing
+// their stop) then waits for the holder to be scheduled again.  Use it only where every job decided or finished under
+// it stays referenced past its scope (a slot's or a local JobP): the deferred list holds plain pointers.
+class PoolLock {
+ public:
+  PoolLock();
+  ~PoolLock();
+  PoolLock(const PoolLock&) = delete;
+  PoolLock& operator=(const PoolLock&) = delete;
+
+ private:
+  std::unique_lock<std::mutex> lk_;
+};
 
 // -- job state transitions (caller holds g_pool.mu; npow_pool.cpp) ------------------------------
 void decide_locked(Job& j, int status, uint64_t nonce = 0, uint64_t value = 0);
 void admit_locked();
 void finish_locked(const JobP& j);
-void device_done_locked(const JobP& j, size_t k);
+// t_seen: when the device's worker observed it stop hashing the job (its final count read), 0 = now
+void device_done_locked(const JobP& j, size_t k, double t_seen = 0.0);
 void abandon_locked(const JobP& j, size_t k, int code, const std::string& msg);
 void stop_other_devices_locked(Job& j, size_t k_win);
 int index_in(const Job& j, int dev);  // the job's index of logical device dev, or -1

@@ -30,7 +30,7 @@ NPOW_ERR_INVALID_WORK = -5
 NPOW_ERR_CAPACITY = -6
 NPOW_ERR_INTERNAL = -7
 
-NPOW_ABI_VERSION = 5
+NPOW_ABI_VERSION = 6
 # hash paths of npow_values_path
 NPOW_PATH_SEARCH = 0   # the stream the search and sweep kernels execute (four 512-lane workgroups per CU)
 NPOW_PATH_SEQ = 1      # a second generated stream, scheduled without barriers
@@ -82,6 +82,9 @@ class DeviceStats(ctypes.Structure):
         ("affinity_checks", ctypes.c_uint64),
         ("affinity_failures", ctypes.c_uint64),
         ("watcher_decisions", ctypes.c_uint64),
+        # ABI 6
+        ("stale_drains", ctypes.c_uint64),
+        ("linger_ms", ctypes.c_double),
     ]
 
 

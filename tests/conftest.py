@@ -22,6 +22,29 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X GPU (libnanopow HIP path)")
 
 
+# Run order of the GPU suite: under `pytest -x` the first failure hides every test after it, and
+# collection is alphabetical by file.  So the bit-exact parity tests and the JSON drop-in go first, then the pool,
+# sanitizers, faults and the BASELINE configs, and the tests whose subject is latency (stop spans, lingering
+# launches) last.  Files not named here keep their place after the named ones, in collection order.
+GPU_ORDER = ["test_gpu_parity.py", "test_gpu_server.py", "test_gpu_kernels.py", "test_gpu_pool.py",
+             "test_gpu_sanitizers.py", "test_gpu_faults.py", "test_gpu_exit.py", "test_gpu_configs.py",
+             "test_gpu_linger.py", "test_gpu_multidevice.py"]
+# ... and within a file these go after the rest of it
+LATENCY_LAST = ("test_first_win_overshoot",)
+
+
+def _order_key(item):
+    fname = os.path.basename(str(item.fspath))
+    rank = GPU_ORDER.index(fname) if fname in GPU_ORDER else len(GPU_ORDER)
+    latency = any(item.name.startswith(p) for p in LATENCY_LAST)
+    return (1 if latency else 0, rank)
+
+
+def pytest_collection_modifyitems(session, config, items):
+    # a stable sort: the order within each (latency, file) group is the collection order
+    items[:] = sorted(items, key=_order_key)
+
+
 def load_golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)

@@ -77,6 +77,12 @@ def main(n_search, which, mask=0):
            "late_equal_share": round(sum(1 for x in late_l if x == late_expected) / len(late_l), 4),
            "late_max": max(late_l),
            "affinity": [sum(x.affinity_checks for x in st), sum(x.affinity_failures for x in st)],
+           # one iteration of each device's grid (one 64-nonce hash per wave, 512 nonces per workgroup) at its kernel
+           # rate over the time it hashed (kernel_ms less its lingering launches' idle waits, npow_device_stats ABI 6)
+           "iteration_us": [round(x.grid * 512 / (x.nonces / max(1e-9, x.kernel_ms - x.linger_ms) / 1e3), 2)
+                            for x in st],
+           "stale_drains": sum(x.stale_drains for x in st),
+           "linger": os.environ.get("NANOPOW_LINGER", "default"),
            "finish_ms_p50": round(pct(ttw, 50) / 1e3, 3),
            "result_ms_p50": round(pct(res_ms, 50), 3),
            "distinct_winners": len(set(winners)), "kills_relayed": kills,

@@ -1,0 +1,67 @@
+"""Process exit with launches in flight.
+
+Round 5 found processes running lingering launches dying with SIGSEGV in their exit handlers under rocprofv3
+(profiles/r05aq_hip_api_trace_overshoot_g4.txt; the bench's regime child, tools/prof_r04.sh): at exit the pool
+workers left at once, and a lingering launch (or a search launch) was still running while the HIP runtime and the
+profiler's tool library tore down.  Since round 6 the exit hook drains like npow_shutdown -- every job cancelled, its
+kill word raised, lingering launches given their yield, every launch retired -- before the runtime's own exit handlers
+run (npow_pool.cpp pool_exit).  Checked here: the overshoot worker with lingering launches forced on over 4 CU
+partitions, and the bench's 8-partition regime child (lingering on by default there), exit with rc 0 on their own and
+under `rocprofv3 --kernel-trace --stats`, each ending while the engine still has launches running (the process exits
+right after its last search, without npow_shutdown).
+Run on an MI355X: ``pytest -m gpu``.
+"""
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+from conftest import ROOT
+
+pytestmark = pytest.mark.gpu
+
+ROCPROF = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+
+
+def _run(cmd, env_extra, profiled, timeout=150):
+    env = dict(os.environ, TMPDIR="/tmp", **env_extra)
+    out_dir = tempfile.mkdtemp(prefix="npow_exit_", dir="/tmp")
+    try:
+        if profiled:
+            if not os.path.exists(ROCPROF):
+                pytest.skip("rocprofv3 not found")
+            cmd = [ROCPROF, "--kernel-trace", "--stats", "-d", out_dir, "-o", "run", "--", *cmd]
+        p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+        traced = []
+        for base, _dirs, files in os.walk(out_dir):
+            traced += [f for f in files if f.endswith(".csv")]
+    finally:
+        shutil.rmtree(out_dir, ignore_errors=True)
+    return p, traced
+
+
+OVERSHOOT = [sys.executable, os.path.join("tests", "overshoot_worker.py"), "100", "receive"]
+LINGER4 = {"NANOPOW_LINGER": "1", "NANOPOW_VIRTUAL_DEVICES": "4"}
+REGIME = [sys.executable, "bench.py", "--workload", "regime", "--gpus", "8", "--steps", "200", "--http-requests", "20"]
+REGIME_ENV = {"NANOPOW_VIRTUAL_DEVICES": "8"}
+
+
+@pytest.mark.parametrize("profiled", [False, True], ids=["plain", "rocprofv3"])
+def test_lingering_overshoot_worker_exits_cleanly(profiled):
+    p, traced = _run(OVERSHOOT, LINGER4, profiled)
+    assert p.returncode == 0, (p.returncode, p.stdout[-1500:], p.stderr[-3000:])
+    assert '"ok": true' in p.stdout
+    if profiled:
+        assert traced, "rocprofv3 wrote no trace"
+
+
+@pytest.mark.parametrize("profiled", [False, True], ids=["plain", "rocprofv3"])
+def test_regime_child_exits_cleanly(profiled):
+    p, traced = _run(REGIME, REGIME_ENV, profiled)
+    assert p.returncode == 0, (p.returncode, p.stdout[-1500:], p.stderr[-3000:])
+    assert "node_ttw_8x_regime" in p.stdout
+    if profiled:
+        assert traced, "rocprofv3 wrote no trace"

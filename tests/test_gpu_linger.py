@@ -111,6 +111,9 @@ def test_time_shared_devices_do_not_linger():
 
 
 TASKS = r"""
+# a 200-ms launch budget: a task or bounded search that waited for a lingering launch to end by itself would take
+# ~200 ms; ended by the worker (end_linger) it takes about its own run time (~1 ms)
+eng.set_pool_tuning(budget_us=200_000)
 root = roots(52, 1)[0]
 eng.sweep(root, 0xffffffc000000000, 0, 1 << 22, device_mask=1)  # first calls load their kernels (~20 ms)
 eng.values(root, 0, 64, device=0)
@@ -143,9 +146,14 @@ print(json.dumps({"times": times, "idle_new_launch": after.launches - before.lau
 """
 
 
+# The bound is the mechanism's, not one box's timing: a quarter of the 200-ms budget the child sets,
+# which a call that waited for the lingering launch to end on its own would exceed; measured ~1-3 ms.
+TASK_BOUND_S = 0.05
+
+
 def test_tasks_and_bounded_searches_do_not_wait_for_a_lingering_launch():
     out = _child({"NANOPOW_LINGER": "1"}, TASKS)
-    assert max(out["times"]["sweep"]) < 0.012 and max(out["times"]["values"]) < 0.012, out
-    assert max(out["times"]["bounded"]) < 0.015, out
+    assert max(out["times"]["sweep"]) < TASK_BOUND_S and max(out["times"]["values"]) < TASK_BOUND_S, out
+    assert max(out["times"]["bounded"]) < TASK_BOUND_S, out
     assert out["idle_new_launch"] == 1 and out["idle_new_dyn"] == 0, out
     assert out["pool"] == [0, 0]

@@ -34,6 +34,48 @@ def test_native_library_is_the_hip_path(gpu_engine):
     assert st.cus >= 1 and st.grid == 4 * st.cus and st.pool_groups == 4
 
 
+def bench_root(i: int) -> bytes:
+    """bench.py's roots R_i = blake2b(b"nanopow-bench" + LE64(i), 32)."""
+    import hashlib
+    return hashlib.blake2b(b"nanopow-bench" + i.to_bytes(8, "little"), digest_size=32).digest()
+
+
+def test_config1_send_difficulty_serial_on_one_gpu(gpu_engine):
+    """BASELINE configs[1] as bench.py runs it: one MI355X, one block hash at a time at the send
+    difficulty fffffff800000000, each search submitted, its result taken at the decision (npow_wait_result, what a
+    work_generate reply carries) and the ticket collected (npow_wait).  Every winner re-validates under hashlib (the
+    reference CPU path), and the sample's nonce counts follow the exponential law of a first hit at p = 2^-29 (a
+    Kolmogorov-Smirnov test against Exp(2^29); the few hundred thousand nonces a launch hashes after its win are 0.1 %
+    of the mean).  Times are recorded, not asserted."""
+    from scipy import stats
+    n = 128
+    done, ttw = [], []
+    for i in range(n):
+        root = bench_root(10_000 + i)
+        t0 = time.perf_counter()
+        t = gpu_engine.submit(root, SEND, start=0, device_mask=1)
+        r = t.wait_result(60)
+        ttw.append(time.perf_counter() - t0)
+        assert r is not None and r.status == _lib.NPOW_OK, i
+        assert oracle.work_value_hashlib(root, r.nonce) == r.value >= SEND, i
+        f = t.wait(60)
+        assert (f.status, f.nonce, f.value) == (r.status, r.nonce, r.value) and f.nonces_done > 0
+        done.append(f.nonces_done)
+    mean = float(1 << 29)
+    ks = stats.kstest(np.array(done, dtype=np.float64), "expon", args=(0, mean))
+    assert ks.pvalue > 1e-3, (ks, np.mean(done) / mean)
+    # the mean within 4.5 standard errors (an exponential's sd is its mean)
+    assert abs(np.mean(done) / mean - 1.0) < 4.5 / np.sqrt(n), np.mean(done) / mean
+    rec = {"test": "config1_send_serial", "searches": n, "ks_pvalue": round(float(ks.pvalue), 4),
+           "mean_nonces_over_2p29": round(float(np.mean(done)) / mean, 4),
+           "ttw_ms_p50": round(float(np.median(ttw)) * 1e3, 3), "ttw_ms_p99": round(float(np.percentile(ttw, 99)) * 1e3, 3)}
+    d = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "latency_records.jsonl"), "a") as fh:
+        import json
+        fh.write(json.dumps(rec) + "\n")
+
+
 PATHS = pytest.mark.parametrize("path", [_lib.NPOW_PATH_SEARCH, _lib.NPOW_PATH_SEQ], ids=["search_stream", "seq_stream"])
 
 
