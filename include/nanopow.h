@@ -62,8 +62,10 @@ extern "C" {
  * npow_device_stats gains idle_ms / idle_gaps (the GPU idle between the device's search launches) and
  * affinity_checks / affinity_failures (NANOPOW_TEST_HOOKS=1, since npow_init: the calling thread's HIP device checked
  * at every HIP call site of the device) and watcher_decisions.  Both structs are still written up to the size the caller passes.
- * 6: npow_device_stats gains stale_drains (a protocol check: won or killed jobs of a lingering launch whose final count
- * never came) and linger_ms (the device's lingering launches waiting with nothing to hash, inside kernel_ms). */
+ * 6: npow_device_stats gains stale_drains / stale_late / stale_missing / stale_gpu_delay_us (won or killed jobs of a
+ * lingering launch whose final count had not come 1 ms after their stop; of those, the ones whose count came later and
+ * the ones whose count never came -- a protocol check: 0), linger_ms (the device's lingering launches waiting with
+ * nothing to hash, inside kernel_ms) and linger_relays (kills relayed by a lingering workgroup). */
 #define NPOW_ABI_VERSION 6
 
 /* Hash paths of npow_values_path. */
@@ -120,9 +122,15 @@ typedef struct npow_device_stats {
                                  over every live slot's record; NANOPOW_WATCHER=0 leaves them to the device's worker) */
   /* ---- ABI 6 ---- */
   uint64_t stale_drains;    /* won or killed jobs of a lingering launch whose final count the kernel had not published
-                               1 ms after the stop (the worker then ended the launch and read the count back): 0 */
+                               1 ms after the stop (the worker then ended the launch and read the count back) */
   double linger_ms;         /* of kernel_ms, the time this device's lingering launches waited with nothing to hash
                                (host-timed): (kernel_ms - linger_ms) is the time the device hashed */
+  uint64_t linger_relays;   /* final counts published after a lingering workgroup relayed the kill of an entry that
+                               no workgroup was hashing (ls2_linger_relay; without it the count never came) */
+  uint64_t stale_late;      /* of stale_drains: the count was published later after all (the GPU was late) ... */
+  uint64_t stale_missing;   /* ... or never, though every launch that held the job ended: a protocol hole, 0 */
+  double stale_gpu_delay_us; /* the latest such late count's publish after the job's deciding win, on the GPU's clock
+                                (s_memrealtime; one clock over CU partitions of one GPU, not across GPUs) */
 } npow_device_stats;
 
 /* Outcome of one search (npow_wait_info).  Times are host steady-clock microseconds since

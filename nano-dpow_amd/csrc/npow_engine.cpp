@@ -451,13 +451,31 @@ int npow_init(int* n_devices) try {
   pool_start();
   static bool exit_hook = false;
   if (!exit_hook) {
-    // Join the pool's worker threads before static destructors run (a joinable std::thread
-    // would terminate the process).  No HIP calls here: by now a profiler or the runtime may
-    // have torn its state down; the OS reclaims device memory with the process.
+    // Process exit without npow_shutdown (round 6).  This hook is registered after the HIP runtime and
+    // any profiler tool library were loaded and initialised, so it runs before their exit handlers and static
+    // destructors (atexit order is the reverse of registration): the HIP runtime is still whole here.  It drains the
+    // pool (pool_exit: jobs cancelled, launches ended and retired, workers joined -- a joinable std::thread would
+    // terminate the process) and then frees every device's streams, events and memory, as npow_shutdown does.  Left
+    // to the runtime's own teardown, the CU-masked streams of NANOPOW_VIRTUAL_DEVICES (and launches still running on
+    // them, round 5) were destroyed after rocprofv3's tool had finalised: SIGSEGV in __cxa_finalize
+    // (profiles/r06a_exit_sigsegv.txt).  The frees run on a thread of their own, as the drain's HIP calls run on the
+    // pool workers: by the time exit() runs the atexit handlers, the calling thread's thread_local objects -- a
+    // profiler's per-thread HIP stream stack among them -- are destroyed, and rocprofv3 aborted on a HIP call made
+    // from it ("Check failed: 'get_stream_stack()' Must be non nullptr", profiles/r06d_exit_regime_tls_abort.txt).
+    // A drain that timed out (a device that stopped answering) frees nothing: hipStreamSynchronize could block the
+    // exit for good.  A device a caller's thread still holds (a sweep in flight at exit) is not freed either.
     exit_hook = true;
     atexit([] {
       std::lock_guard<std::mutex> g(g_mu);
-      if (g_init) pool_exit();
+      if (!g_init) return;
+      if (!pool_exit()) return;
+      std::thread([] {
+        for (auto& d : g_devs) {
+          std::unique_lock<std::mutex> lk(d->mu, std::try_to_lock);
+          if (lk.owns_lock()) free_device(*d);
+        }
+      }).join();
+      g_init = false;
     });
   }
   if (n_devices) *n_devices = (int)g_devs.size();
@@ -570,6 +588,10 @@ static int stats_fill(int device, npow_device_stats* out) {
   out->affinity_failures = d.affinity_failures.load(std::memory_order_relaxed);
   out->watcher_decisions = d.watcher_decisions;
   out->stale_drains = d.stale_drains;
+  out->linger_relays = d.linger_relays;
+  out->stale_late = d.stale_late;
+  out->stale_missing = d.stale_missing;
+  out->stale_gpu_delay_us = d.stale_gpu_delay_us;
   out->linger_ms = d.linger_ms;
   return NPOW_OK;
 }
@@ -599,8 +621,8 @@ int npow_device_stats_reset(int device) try {
   const double cpu = worker_cpu_ms(d);
   std::lock_guard<std::mutex> g(d.stats_mu);
   d.launches = d.nonces = d.invalid = d.early = d.early_mismatch = d.yields = d.dyn = d.kills_relayed = d.late = 0;
-  d.idle_gaps = d.watcher_decisions = d.stale_drains = 0;
-  d.idle_ms = d.linger_ms = 0.0;
+  d.idle_gaps = d.watcher_decisions = d.stale_drains = d.linger_relays = d.stale_late = d.stale_missing = 0;
+  d.idle_ms = d.linger_ms = d.stale_gpu_delay_us = 0.0;
   d.kernel_ms = 0.0;
   d.clk_ticks = d.clk_ref_ticks = 0.0;
   d.stats_t0 = std::chrono::steady_clock::now();

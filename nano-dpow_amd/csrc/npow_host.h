@@ -68,7 +68,12 @@ struct Device {
   uint64_t kills_relayed = 0;              // losing jobs stopped by another device's decision (npow_pool.cpp)
   uint64_t late = 0;                       // device-side overshoot: nonces hashed after the job was known over
   uint64_t watcher_decisions = 0;          // jobs the win watcher decided from this device's win records
-  uint64_t stale_drains = 0;               // won / killed slots of a lingering launch whose final count never came
+  uint64_t stale_drains = 0;               // won / killed slots of a lingering launch whose final count had not come
+                                           // 1 ms after their stop (the worker then ended the launch) ...
+  uint64_t stale_late = 0;                 // ... of which the count came later after all ...
+  uint64_t stale_missing = 0;              // ... or never, though every launch holding the slot ended (a protocol hole)
+  double stale_gpu_delay_us = 0.0;         // the latest late count's publish after the job's deciding win (GPU clock)
+  uint64_t linger_relays = 0;              // final counts that followed a kill relayed by a lingering workgroup
   double linger_ms = 0.0;                  // host-timed waits of lingering launches with nothing to hash (in kernel_ms)
   double idle_ms = 0.0;                    // GPU idle between consecutive search launches (HIP events) ...
   uint64_t idle_gaps = 0;                  // ... over this many pairs (npow_pool.cpp Worker::retire)
@@ -188,7 +193,7 @@ int pool_device_init(Device& d);     // allocate pool buffers of one device
 void pool_device_free(Device& d);
 void pool_start();                   // start one worker thread per device
 void pool_stop();                    // stop and join the workers (pending jobs end with an error)
-void pool_exit();                    // process exit: join the workers without further HIP calls
+bool pool_exit();                    // process exit: drain and join the workers (bounded); false: the drain timed out
 int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint64_t device_mask,
                 uint64_t max_nonces_per_device, const volatile uint32_t* cancel, uint64_t* ticket);
 // info (may be null): the search's timeline and overshoot (npow_wait_info)

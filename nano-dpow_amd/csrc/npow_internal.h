@@ -226,8 +226,11 @@ struct alignas(64) PoolFin {
   uint64_t t_fin;    // s_memrealtime of the publication (NANOPOW_TRACE_LATENCY GPU timelines)
   uint64_t t_relay;  // diagnostic builds (-DNPOW_DIAG_TIMES): s_memrealtime when a poll read the slot's kill word
   uint64_t t_join;   // ... and when a workgroup last started hashing the slot's entry
-  uint8_t pad[16];
+  uint64_t linger_gen;  // round 6: the generation whose kill a lingering workgroup relayed (ls2_linger_relay) --
+                        // an entry left live with no workgroup on it; the host counts them (stats linger_relays)
+  uint8_t pad[8];
 };
+static_assert(sizeof(PoolFin) == 64, "one line per slot");
 // An unbounded job adopted while a search launch runs joins that launch instead of ending it
 // (a yield): the host writes its entry at ring position p (dyn[p % kDynRing]) and then releases
 // the low half of PoolMailbox::ctl = p + 1; the launch's entries are its table's n entries followed by positions

@@ -778,8 +778,11 @@ __device__ __forceinline__ void ls2_linger_relay(const PoolTable* tab, PoolDevSt
     if ((over >> k) & 1) continue;
     const EntryHdr q = ls2_hdr(tab, mb, k);
     if (load_dead(st, q.slot) < q.gen &&
-        __hip_atomic_load(&mb->kill[q.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q.gen)
+        __hip_atomic_load(&mb->kill[q.slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == q.gen) {
+      // (marked before the kill, whose publish releases the final count: the host reads it with the record)
+      __hip_atomic_store(&mb->fin[q.slot].linger_gen, q.gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       ls2_kill(st, mb, q.slot, q.gen, true);  // (a lingering launch is counted)
+    }
   }
   __hip_atomic_store(kd, key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }

@@ -669,6 +669,16 @@ class Worker {
   void handle_win(int s);
   bool win_published(int s) const;
   void early_finish(int s);
+  // A stale slot's final count came after all (late): how late on the GPU's clock, after the job's deciding win
+  // (npow_device_stats.stale_gpu_delay_us; one clock for CU partitions of one GPU)
+  void stale_fin_came(int s) {
+    const Slot& sl = slots_[s];
+    const uint64_t tf = __atomic_load_n(&d_.pmb->fin[s].t_fin, __ATOMIC_RELAXED);
+    const uint64_t tw = sl.job ? sl.job->gpu_t_win : 0;
+    std::lock_guard<std::mutex> sg(d_.stats_mu);
+    d_.stale_late++;
+    if (tw && tf > tw) d_.stale_gpu_delay_us = std::max(d_.stale_gpu_delay_us, (double)(tf - tw) / 100.0);
+  }
   void publish_busy() {
     int active = 0;
     for (const Slot& s : slots_) active += s.state == SlotState::kActive ? 1 : 0;
@@ -1005,6 +1015,11 @@ void Worker::early_finish(int s) {
     }
 #endif
   }
+  if (__atomic_load_n(&d_.pmb->fin[s].linger_gen, __ATOMIC_RELAXED) == sl.gen) {  // relayed by a lingering workgroup
+    std::lock_guard<std::mutex> sg(d_.stats_mu);
+    d_.linger_relays++;
+  }
+  if (sl.stale) stale_fin_came(s);
   if (d_.dead || sl.requeue || !j.decided.load()) return;
   sl.early = true;
   const uint64_t delta = total - sl.baseline;
@@ -1350,6 +1365,14 @@ int Worker::retire() {
       d_.late += late_delta;
     }
     if (win_published(s)) handle_win(s);  // published by the last launch, not yet seen
+    if (sl.stale && !sl.fin_seen) {  // every launch that held it has ended: its count came late, or never
+      if (__atomic_load_n(&d_.pmb->fin[s].gen, __ATOMIC_ACQUIRE) == sl.gen) {
+        stale_fin_came(s);
+      } else {
+        std::lock_guard<std::mutex> sg(d_.stats_mu);
+        d_.stale_missing++;
+      }
+    }
     NPOW_DBG("nanopow[%d]: retire slot %d g%llu done %llu requeue %d early %d\n", d_.id, s,
              (unsigned long long)sl.gen, (unsigned long long)delta, (int)sl.requeue, (int)sl.early);
     if (sl.early) {  // finished by early_finish(): the read-back must add nothing to its count
@@ -1429,7 +1452,8 @@ int Worker::step() {
       if (sl.state != SlotState::kDraining || sl.fin_seen || sl.inflight.empty()) continue;
       if (sl.stop_us > 0 && t - sl.stop_us > g_linger_us) {
         stale = true;
-        if (!sl.stale && lingering) {  // the fallback below fires for it: counted (tests assert it stays 0)
+        if (!sl.stale && lingering) {  // the fallback below fires for it: counted, and classified when the slot's count
+                                       // comes late or not at all (early_finish / retire: stale_missing)
           sl.stale = true;
           std::lock_guard<std::mutex> sg(d_.stats_mu);
           d_.stale_drains++;
@@ -1675,10 +1699,12 @@ void pool_start() {
 // regardless.  The hook runs before the HIP runtime's own exit handlers (it was registered after the runtime was
 // loaded and initialised: atexit runs in reverse order), so the workers' HIP calls (event queries) are still valid.
 constexpr double kExitDrainMs = 250.0;
-void pool_exit() {
+bool pool_exit() {
   g_exit_deadline_us.store(now_us() + kExitDrainMs * 1e3);
   pool_stop();
+  const bool drained = !g_exiting.load();  // (set only by exit_now() once the deadline passed)
   g_exiting = true;
+  return drained;
 }
 
 void pool_stop() {

@@ -85,6 +85,10 @@ class DeviceStats(ctypes.Structure):
         # ABI 6
         ("stale_drains", ctypes.c_uint64),
         ("linger_ms", ctypes.c_double),
+        ("linger_relays", ctypes.c_uint64),
+        ("stale_late", ctypes.c_uint64),
+        ("stale_missing", ctypes.c_uint64),
+        ("stale_gpu_delay_us", ctypes.c_double),
     ]
 
 

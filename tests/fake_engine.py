@@ -67,7 +67,8 @@ class OracleEngine:
                                clock_mhz=0.0, early_finishes=0, kills_relayed=0, host_cpu_ms=0.0,
                                host_wall_ms=1.0, grid=0, pool_groups=4, late_nonces=0, hip_device=0,
                                cu_first=-1, cus=256, idle_ms=0.0, idle_gaps=0, affinity_checks=0, affinity_failures=0,
-                               watcher_decisions=0, dyn_entries=0, stale_drains=0, linger_ms=0.0)
+                               watcher_decisions=0, dyn_entries=0, stale_drains=0, linger_ms=0.0, linger_relays=0,
+                               stale_late=0, stale_missing=0, stale_gpu_delay_us=0.0)
 
     def version(self):
         return "oracle stand-in engine (tests/fake_engine.py)"

@@ -82,6 +82,9 @@ def main(n_search, which, mask=0):
            "iteration_us": [round(x.grid * 512 / (x.nonces / max(1e-9, x.kernel_ms - x.linger_ms) / 1e3), 2)
                             for x in st],
            "stale_drains": sum(x.stale_drains for x in st),
+           "linger_relays": sum(x.linger_relays for x in st),
+           "stale_late": sum(x.stale_late for x in st), "stale_missing": sum(x.stale_missing for x in st),
+           "stale_gpu_delay_us": round(max(x.stale_gpu_delay_us for x in st), 1),
            "linger": os.environ.get("NANOPOW_LINGER", "default"),
            "finish_ms_p50": round(pct(ttw, 50) / 1e3, 3),
            "result_ms_p50": round(pct(res_ms, 50), 3),

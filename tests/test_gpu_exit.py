@@ -5,10 +5,13 @@ Round 5 found processes running lingering launches dying with SIGSEGV in their e
 workers left at once, and a lingering launch (or a search launch) was still running while the HIP runtime and the
 profiler's tool library tore down.  Since round 6 the exit hook drains like npow_shutdown -- every job cancelled, its
 kill word raised, lingering launches given their yield, every launch retired -- before the runtime's own exit handlers
-run (npow_pool.cpp pool_exit).  Checked here: the overshoot worker with lingering launches forced on over 4 CU
-partitions, and the bench's 8-partition regime child (lingering on by default there), exit with rc 0 on their own and
-under `rocprofv3 --kernel-trace --stats`, each ending while the engine still has launches running (the process exits
-right after its last search, without npow_shutdown).
+run, and then frees every device's streams, events and memory as npow_shutdown does (npow_pool.cpp pool_exit,
+npow_engine.cpp's exit hook): round 6's first run showed the crash with the drain alone -- after rocprofv3's tool
+finalisation, in a static destructor (profiles/r06a_exit_sigsegv.txt), i.e. in the runtime's teardown of the process's
+CU-masked streams.  Checked here: the overshoot worker over 4 CU partitions with lingering launches forced on and off,
+and the bench's 8-partition regime child (lingering on by default there), exit with rc 0 on their own and under
+`rocprofv3 --kernel-trace --stats`, each ending while the engine still has launches running (the process exits right
+after its last search, without npow_shutdown).
 Run on an MI355X: ``pytest -m gpu``.
 """
 import os
@@ -33,8 +36,13 @@ def _run(cmd, env_extra, profiled, timeout=150):
         if profiled:
             if not os.path.exists(ROCPROF):
                 pytest.skip("rocprofv3 not found")
-            cmd = [ROCPROF, "--kernel-trace", "--stats", "-d", out_dir, "-o", "run", "--", *cmd]
-        p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+            cmd = [ROCPROF, "--kernel-trace", "--stats", "--output-format", "csv", "-d", out_dir, "-o", "run", "--", *cmd]
+        try:
+            p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+        except subprocess.TimeoutExpired as e:  # (a hang at exit: report what it printed)
+            err = e.stderr.decode(errors="replace") if isinstance(e.stderr, bytes) else (e.stderr or "")
+            out = e.stdout.decode(errors="replace") if isinstance(e.stdout, bytes) else (e.stdout or "")
+            pytest.fail(f"timed out after {timeout} s; stdout {out[-600:]!r}; stderr {err[-4000:]!r}")
         traced = []
         for base, _dirs, files in os.walk(out_dir):
             traced += [f for f in files if f.endswith(".csv")]
@@ -44,14 +52,16 @@ def _run(cmd, env_extra, profiled, timeout=150):
 
 
 OVERSHOOT = [sys.executable, os.path.join("tests", "overshoot_worker.py"), "100", "receive"]
-LINGER4 = {"NANOPOW_LINGER": "1", "NANOPOW_VIRTUAL_DEVICES": "4"}
+PARTITIONS = {"linger4": {"NANOPOW_LINGER": "1", "NANOPOW_VIRTUAL_DEVICES": "4"},   # lingering launches at exit
+              "cu4": {"NANOPOW_LINGER": "0", "NANOPOW_VIRTUAL_DEVICES": "4"}}      # CU-masked streams, no lingering
 REGIME = [sys.executable, "bench.py", "--workload", "regime", "--gpus", "8", "--steps", "200", "--http-requests", "20"]
 REGIME_ENV = {"NANOPOW_VIRTUAL_DEVICES": "8"}
 
 
 @pytest.mark.parametrize("profiled", [False, True], ids=["plain", "rocprofv3"])
-def test_lingering_overshoot_worker_exits_cleanly(profiled):
-    p, traced = _run(OVERSHOOT, LINGER4, profiled)
+@pytest.mark.parametrize("parts", sorted(PARTITIONS))
+def test_partitioned_overshoot_worker_exits_cleanly(parts, profiled):
+    p, traced = _run(OVERSHOOT, PARTITIONS[parts], profiled)
     assert p.returncode == 0, (p.returncode, p.stdout[-1500:], p.stderr[-3000:])
     assert '"ok": true' in p.stdout
     if profiled:
