@@ -1310,6 +1310,18 @@ def run_timed_inprocess(eng, n_dev: int, steps: int, warmup: int, thr: int = SEN
             sum(k.nonces for k in ks), sum(k.launches for k in ks), ks)
 
 
+def busy_ms(k) -> float:
+    """A device's HIP-event kernel time less what its lingering launches spent waiting with nothing to hash
+    (npow_device_stats.linger_ms, ABI 6; 0 from older libraries): the time it hashed."""
+    return max(0.0, k.kernel_ms - getattr(k, "linger_ms", 0.0))
+
+
+def hash_rate(k) -> float:
+    """Nonces per second over the time the device hashed (busy_ms); 0 before its first launch."""
+    b = busy_ms(k)
+    return k.nonces / (b * 1e-3) if b > 0 else 0.0
+
+
 def device_check(rates, kernel_nonces, search_nonces, clocks=None):
     """a multi-GPU run fails loudly rather than reporting a node rate with a slow or miscounting
     device in it -- every device's kernel rate within 0.9x of the median, and the devices' nonce counters
@@ -1454,7 +1466,7 @@ def node_regime(eng, n_dev: int, m: int, thr: int = REGIME, http_m: int = 0):
         raise RuntimeError("; ".join(errors[:4]))
     ks = [eng.stats(d) for d in range(n_dev)]
     done = [x.nonces_done for x in infos]
-    kern_rate = sum(k.nonces / (k.kernel_ms * 1e-3) for k in ks if k.kernel_ms > 0)  # node: devices side by side
+    kern_rate = sum(hash_rate(k) for k in ks)  # node: devices side by side (lingering waits left out: busy_ms)
     node_gnps = sum(done) / wall / 1e9
     ln2 = 0.6931471805599453
     E = float(1 << 64) / float((1 << 64) - thr)
@@ -1509,8 +1521,8 @@ def node_regime(eng, n_dev: int, m: int, thr: int = REGIME, http_m: int = 0):
         "launches_per_search_per_device": round(sum(k.launches for k in ks) / (m * n_dev), 3),
         "dyn_entries_per_search_per_device": round(sum(k.dyn_entries for k in ks) / (m * n_dev), 3),
         "late_nonces_losers": _mean_p([x.late_nonces_losers for x in infos]),
-        "per_device_kernel_gnps": [round(k.nonces / (k.kernel_ms * 1e-3) / 1e9, 4) if k.kernel_ms > 0 else None
-                                   for k in ks],
+        "per_device_kernel_gnps": [round(hash_rate(k) / 1e9, 4) if k.kernel_ms > 0 else None for k in ks],
+        "per_device_linger_ms": [round(getattr(k, "linger_ms", 0.0), 2) for k in ks],
         "in_kernel_mhz": round(statistics.mean([k.clock_mhz for k in ks if k.clock_mhz > 0]), 1)
         if any(k.clock_mhz > 0 for k in ks) else None,
         "worker_core_share": round(sum(k.host_cpu_ms for k in ks) / max(1e-9, ks[0].host_wall_ms), 3),
@@ -1759,8 +1771,9 @@ def main_inprocess(eng, args) -> int:
                 "those of separate GPUs (a rehearsal of the path)")
     line["early_finishes"] = sum(k.early_finishes for k in ks)
     line["kills_relayed"] = sum(k.kills_relayed for k in ks)
-    line["device_check"] = device_check([k.nonces / (k.kernel_ms * 1e-3) / 1e9 if k.kernel_ms > 0 else 0.0 for k in ks],
-                                        kern_nonces, nonces, [k.clock_mhz for k in ks])
+    # rates over the time each device hashed: a CU partition that lingered more is not slower
+    line["device_check"] = device_check([hash_rate(k) / 1e9 for k in ks], kern_nonces, nonces,
+                                        [k.clock_mhz for k in ks])
     if args.node_searches:
         line["node_ttw_ms"] = inprocess_node_ttw(eng, n, args.node_searches)
     print(json.dumps(line), flush=True)

@@ -1450,7 +1450,10 @@ int Worker::step() {
     for (const PoolInflight& f : q_) lingering = lingering || f.linger;
     for (Slot& sl : slots_) {
       if (sl.state != SlotState::kDraining || sl.fin_seen || sl.inflight.empty()) continue;
-      if (sl.stop_us > 0 && t - sl.stop_us > g_linger_us) {
+      // (the record read again after t: a worker descheduled for a millisecond between check_slots' look and here
+      // would otherwise count a count that came meanwhile as stale -- round 6 saw 8 at once over 8 partitions)
+      if (sl.stop_us > 0 && t - sl.stop_us > g_linger_us &&
+          __atomic_load_n(&d_.pmb->fin[&sl - slots_].gen, __ATOMIC_ACQUIRE) != sl.gen) {
         stale = true;
         if (!sl.stale && lingering) {  // the fallback below fires for it: counted, and classified when the slot's count
                                        // comes late or not at all (early_finish / retire: stale_missing)

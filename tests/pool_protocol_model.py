@@ -38,8 +38,8 @@ import dataclasses
 from typing import Dict, List, Optional, Tuple
 
 N_ENT = 2
-HASH_CAP = 2   # hashes counted per segment (more add nothing new to the protocol: a workgroup that keeps hashing
-               # keeps the same counts and can still take every other step)
+HASH_CAP = 1   # hashes counted per segment: 0 or 1 tells a workgroup that hashed from one that did not, which is all the
+               # protocol's counts can tell apart (more multiplies the states; 2 was checked too, tests/test_pool_...)
 
 
 @dataclasses.dataclass(frozen=True)
@@ -195,10 +195,11 @@ class Model:
                 return [("choose-none", sh, L(pc="LOOK", looked=fail_looked, over=new_over, e=-1, sub=None))]
             m = min(wgs[i][s] for i in live)
             for i in live:
-                if wgs[i][s] == m:
-                    out.append((f"join{i}", _repl(sh, wgs=_inc(wgs, i, s, +1)),
-                                L(pc="JOINCHK", e=i, over=new_over, local=0, stop=0, end=0)))
+                if wgs[i][s] == m:  # the pick (lanes' reads); lane 0's join is the next step
+                    out.append((f"pick{i}", sh, L(pc="JOINADD", e=i, over=new_over, local=0, stop=0, end=0)))
             return out
+        if pc == "JOINADD":
+            return [(f"join{e}", _repl(sh, wgs=_inc(wgs, e, s, +1)), L(pc="JOINCHK"))]
         if pc == "JOINCHK":
             if cfg.bug_join_no_recheck:
                 return [("join-nocheck", sh, L(pc="HASH"))]
@@ -352,7 +353,7 @@ class Result:
     violations: List[Tuple[str, list]]
 
 
-def check(cfg: Config, max_states: int = 3_000_000, want_trace: bool = True) -> Result:
+def check(cfg: Config, max_states: int = 3_000_000, want_trace: bool = True, stop_at_first: bool = False) -> Result:
     """Every interleaving, by DFS over the explicit states (deduplicated), then the properties:
     EXACT on every state; FIN as reachability -- from every state where the workgroups all linger or have exited,
     some linger, and an entry is won or killed without its final count, a state with that count published must be
@@ -381,7 +382,7 @@ def check(cfg: Config, max_states: int = 3_000_000, want_trace: bool = True) -> 
             kinds.add(kind)
             violations.append((kind, trace(st) if want_trace else []))
 
-    while stack:
+    while stack and not (stop_at_first and violations):
         st = stack.pop()
         sh, locs = st
         dead, wgs, done, fin, kill, kills, kd, nd, yld, mirror, budget, won, khost = sh
