@@ -150,8 +150,8 @@ def issue_bound_cycles(mix):
     full = mix["valu"] - adds - aligns
     return 4 * (adds + aligns + max(0, full - aligns) / 2)
 # rocprofv3 PMC passes of the bench's own command (tools/pmc_bench.sh), newest first
-PMC_POOL = ("r05av_pmc_pool.json", "r05au_pmc_pool.json", "r05am_pmc_pool.json", "r05ak_pmc_pool.json", "r05f_pmc_pool.json", "r04j_pmc_pool.json", "r04i_pmc_pool.json", "r04h_pmc_pool.json", "r04g_pmc_pool.json", "r04f_pmc_pool.json", "r04e_pmc_pool.json", "r03s_pmc_pool.json", "r03w_pmc_pool.json", "r03p_pmc_pool.json", "r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
-PMC_SWEEP = ("r05av_pmc_sweep.json", "r05au_pmc_sweep.json", "r05am_pmc_sweep.json", "r05ak_pmc_sweep.json", "r05f_pmc_sweep.json", "r04j_pmc_sweep.json", "r04i_pmc_sweep.json", "r04h_pmc_sweep.json", "r04g_pmc_sweep.json", "r04f_pmc_sweep.json", "r04e_pmc_sweep.json", "r03s_pmc_sweep.json", "r03w_pmc_sweep.json", "r03p_pmc_sweep.json", "r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
+PMC_POOL = ("r06f_pmc_pool.json", "r05av_pmc_pool.json", "r05au_pmc_pool.json", "r05am_pmc_pool.json", "r05ak_pmc_pool.json", "r05f_pmc_pool.json", "r04j_pmc_pool.json", "r04i_pmc_pool.json", "r04h_pmc_pool.json", "r04g_pmc_pool.json", "r04f_pmc_pool.json", "r04e_pmc_pool.json", "r03s_pmc_pool.json", "r03w_pmc_pool.json", "r03p_pmc_pool.json", "r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
+PMC_SWEEP = ("r06f_pmc_sweep.json", "r05av_pmc_sweep.json", "r05au_pmc_sweep.json", "r05am_pmc_sweep.json", "r05ak_pmc_sweep.json", "r05f_pmc_sweep.json", "r04j_pmc_sweep.json", "r04i_pmc_sweep.json", "r04h_pmc_sweep.json", "r04g_pmc_sweep.json", "r04f_pmc_sweep.json", "r04e_pmc_sweep.json", "r03s_pmc_sweep.json", "r03w_pmc_sweep.json", "r03p_pmc_sweep.json", "r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
 METRIC = "Gnonce/s blake2b-64 per GPU & 8-GPU node; p50 time-to-work at fffffff8"
 CSRC = os.path.join(HERE, "nano-dpow_amd", "csrc")
 
@@ -1523,6 +1523,11 @@ def node_regime(eng, n_dev: int, m: int, thr: int = REGIME, http_m: int = 0):
         "late_nonces_losers": _mean_p([x.late_nonces_losers for x in infos]),
         "per_device_kernel_gnps": [round(hash_rate(k) / 1e9, 4) if k.kernel_ms > 0 else None for k in ks],
         "per_device_linger_ms": [round(getattr(k, "linger_ms", 0.0), 2) for k in ks],
+        # the worker's 1-ms fallback for a final count that had not come (ABI 6): late ones, and missing ones (0)
+        "stale_final_counts": {"stale": sum(getattr(k, "stale_drains", 0) for k in ks),
+                               "late": sum(getattr(k, "stale_late", 0) for k in ks),
+                               "missing": sum(getattr(k, "stale_missing", 0) for k in ks),
+                               "linger_relays": sum(getattr(k, "linger_relays", 0) for k in ks)},
         "in_kernel_mhz": round(statistics.mean([k.clock_mhz for k in ks if k.clock_mhz > 0]), 1)
         if any(k.clock_mhz > 0 for k in ks) else None,
         "worker_core_share": round(sum(k.host_cpu_ms for k in ks) / max(1e-9, ks[0].host_wall_ms), 3),

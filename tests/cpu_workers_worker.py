@@ -130,6 +130,25 @@ def main():
         assert e.code == _lib.NPOW_ERR_BAD_ARGUMENT
     st = eng.stats(cpu)
     out["cpu_rate_mnps"] = round(st.nonces / max(st.kernel_ms, 1e-9) / 1e3, 2)
+    # 8. the CPU device's rate alone and beside an endless GPU search (the win watcher spun a core for as
+    #    long as a GPU slot was armed, next to the CPU hashing threads): recorded, not asserted (a timing)
+    def cpu_rate(with_gpu):
+        gtok = _lib.CancelToken()
+        g = eng.submit(bytes(range(50, 82)), M64, device_mask=1, cancel=gtok) if with_gpu else None
+        time.sleep(0.05)
+        eng.reset_stats(cpu)
+        ctok = _lib.CancelToken()
+        c = eng.submit(bytes(range(60, 92)), M64, device_mask=cmask, cancel=ctok)
+        time.sleep(0.5)
+        ctok.set()
+        c.wait(10)
+        s2 = eng.stats(cpu)
+        if g is not None:
+            gtok.set()
+            g.wait(10)
+        return s2.nonces / max(s2.kernel_ms, 1e-9) / 1e3
+    alone, beside = cpu_rate(False), cpu_rate(True)
+    out["cpu_rate_alone_vs_beside_gpu_mnps"] = [round(alone, 2), round(beside, 2), round(beside / max(alone, 1e-9), 3)]
     out["ok"] = True
     print(json.dumps(out), flush=True)
 

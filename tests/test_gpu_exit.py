@@ -73,5 +73,8 @@ def test_regime_child_exits_cleanly(profiled):
     p, traced = _run(REGIME, REGIME_ENV, profiled)
     assert p.returncode == 0, (p.returncode, p.stdout[-1500:], p.stderr[-3000:])
     assert "node_ttw_8x_regime" in p.stdout
+    import json
+    rec = json.loads(p.stdout.strip().splitlines()[-1])["node_ttw_8x_regime"]
+    assert rec["stale_final_counts"]["missing"] == 0, rec["stale_final_counts"]  # no final count lost
     if profiled:
         assert traced, "rocprofv3 wrote no trace"

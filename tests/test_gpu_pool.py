@@ -365,3 +365,23 @@ def test_wait_result_returns_at_the_decision(gpu_engine):
     assert t.wait_result(30).status == _lib.NPOW_EXHAUSTED
     f = t.wait(30)
     assert f.status == _lib.NPOW_EXHAUSTED and f.nonces_done == 100_000
+
+
+def test_a_long_search_does_not_spin_a_core(gpu_engine):
+    """the win watcher spun one core for as long as any slot was armed (a whole long search, an idle
+    lingering launch), and result waiters spun up to 50 ms per call.  Now it spins only for 2 ms after an arm or a
+    record it handled, and waiters for 2 ms: over a second of an endless search nobody waits on, the process uses a
+    fraction of a core (the pool worker's naps and the watcher's 20-us naps), not the one a spinning thread costs."""
+    tok = _lib.CancelToken()
+    t = gpu_engine.submit(bytes(range(100, 132)), M64, device_mask=1, cancel=tok)
+    try:
+        time.sleep(0.1)
+        c0, w0 = time.process_time(), time.perf_counter()
+        time.sleep(1.0)
+        cores = (time.process_time() - c0) / (time.perf_counter() - w0)
+    finally:
+        tok.set()
+    assert t.wait(10).status == _lib.NPOW_CANCELLED
+    print({"process_cores_during_search": round(cores, 3)})
+    assert cores < 0.75, cores
+
