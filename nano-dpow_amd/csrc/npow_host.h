@@ -94,6 +94,7 @@ struct Device {
   std::atomic<uint64_t> armed_mask{0};
   std::atomic<uint64_t> armed_gen[kMaxSlots] = {};
   std::atomic<const volatile uint32_t*> armed_cancel[kMaxSlots] = {};  // the job's caller-owned cancel word, if any
+  std::atomic<double> armed_spin_until[kMaxSlots] = {};  // steady-clock us until which the watcher spins for the slot
   std::mutex armed_mu;
   std::shared_ptr<void> armed_job[kMaxSlots];  // JobP (npow_pool.h), type-erased here
   double kernel_ms = 0.0;

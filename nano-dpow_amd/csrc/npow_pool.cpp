@@ -404,12 +404,19 @@ bool wants_device_locked(int dev) {
 // device's invalid streak and the slot's retirement stay its business; a job already decided is left alone).
 // It also watches each armed job's cancel word (a caller's work_cancel, or another rank's first win through a shared
 // word, bench.py node_time_to_work) and wakes the device's worker at once, which then stops the job's waves.
-// Spinning is bounded (round 6): the watcher spins for kWatchSpinUs after a slot was armed or a record
-// changed -- a receive-difficulty search is won well within that -- and then naps g_watch_nap_us at a time (1-us timer
-// slack; an arm wakes it at once), so a long search, or an idle lingering launch, costs a fraction of a core instead
-// of all of it, and a CPU device's hashing threads (--cpu-threads) keep their cores.  NANOPOW_WATCH_NAP_US=0 spins.
+// Spinning is bounded (round 6): the watcher spins while a job armed on a slot is within its spin window
+// -- three times the job's expected time to a win at its devices' rate (a win comes in it with probability 0.95),
+// at least kWatchSpinUs, at most kWatchSpinMaxUs; kWatchSpinUs only when a CPU device's hashing threads share the host
+// (--cpu-threads) -- or within kWatchSpinUs of a record it handled, and otherwise naps g_watch_nap_us at a time (1-us
+// timer slack).  So an endless or very hard search, or an idle lingering launch, costs a fraction of a core instead of
+// all of it, while a search of the expected length (the serial client's, 2-15 ms at fffffff8 on 8 GPUs or on one)
+// is watched spinning: a flat 2-ms window had put the nap's delay (~10-15 us) on every search longer than 2 ms -- the
+// 8-GPU time regime's fixed cost per search 6 -> 16 us on one GPU (profiles/r06f_regime1.json).
+// NANOPOW_WATCH_NAP_US=0 spins always.
 namespace {
 constexpr double kWatchSpinUs = 2000.0;
+constexpr double kWatchSpinMaxUs = 50000.0;
+constexpr double kNoncesPerCuUs = 139.0;  // a CU's search rate (35.6 Gnonce/s over 256 CUs)
 const double g_watch_nap_us = [] {
   const char* e = getenv("NANOPOW_WATCH_NAP_US");
   return e ? atof(e) : 20.0;
@@ -425,8 +432,24 @@ struct Watch {
 Watch g_watch;
 }  // namespace
 
+// The slot's spin window (above): 3 x the job's expected nonces to a win / its GPU devices' rate, in [2, 50] ms.
+static double spin_window_us(const Job& j) {
+  bool cpu_device = false;
+  double rate = 0.0;  // nonces per us
+  for (const auto& dp : g_devs) cpu_device = cpu_device || dp->cpu_threads > 0;
+  if (cpu_device) return kWatchSpinUs;
+  for (int id : j.devs) {
+    const Device& d = *g_devs[(size_t)id];
+    if (!d.cpu_threads) rate += d.cus * kNoncesPerCuUs;
+  }
+  const double expect = 18446744073709551616.0 / (18446744073709551616.0 - (double)j.threshold + 1.0);
+  const double w = rate > 0 ? 3.0 * expect / rate : kWatchSpinMaxUs;
+  return std::min(kWatchSpinMaxUs, std::max(kWatchSpinUs, w));
+}
+
 void watch_arm(Device& d, int s, uint64_t gen, const JobP& j) {
   if (!g_watcher_on) return;
+  d.armed_spin_until[s].store(now_us() + j->spin_us, std::memory_order_relaxed);
   {
     std::lock_guard<std::mutex> g(d.armed_mu);
     d.armed_job[s] = j;
@@ -517,10 +540,14 @@ void watcher_run() {
     if ((round & 63u) == 0) {  // (the clock every 64 rounds: a round over a few armed slots is ~0.1 us)
       const uint64_t a = g_watch.arms.load(std::memory_order_acquire);
       const double t = now_us();
+      double until = t_event + kWatchSpinUs;  // the armed slots' spin windows (watch_arm)
+      for (const auto& dp : g_devs) {
+        for (uint64_t m = dp->armed_mask.load(std::memory_order_acquire); m; m &= m - 1)
+          until = std::max(until, dp->armed_spin_until[__builtin_ctzll(m)].load(std::memory_order_relaxed));
+      }
       if (a != arms_seen) {
         arms_seen = a;
-        t_event = t;
-      } else if (g_watch_nap_us > 0 && t - t_event > kWatchSpinUs) {
+      } else if (g_watch_nap_us > 0 && t > until) {
         std::unique_lock<std::mutex> lk(g_watch.mu);
         g_watch.cv.wait_for(lk, std::chrono::duration<double, std::micro>(g_watch_nap_us), [&] {
           return g_watch.stop || g_watch.arms.load(std::memory_order_acquire) != arms_seen;
@@ -1781,6 +1808,7 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
   j->t_launch_dev.assign(G, 0.0);
   j->late.assign(G, 0);
   j->pending_devs = (int)G;
+  j->spin_us = spin_window_us(*j);
   j->t_submit = now_us();
   std::lock_guard<std::mutex> g(g_pool.mu);
   if (!g_pool.running) return fail(NPOW_ERR_NOT_INITIALISED, "engine is shut down");
@@ -1793,11 +1821,12 @@ int pool_submit(const uint8_t root[32], uint64_t threshold, uint64_t start, uint
 }
 
 // Waiters of a search's outcome (npow_wait_result) poll instead of sleeping while at most kMaxSpinners of them do,
-// for up to kSpinUs per call: a serial client's reply then leaves as soon as the job is decided instead of after a
-// condition-variable wake-up (decided -> result in the client p50 11 us).  One core each while
-// they do; NANOPOW_WAIT_SPIN=0 turns it off (A/B runs).
+// for up to the job's spin window per call (Job::spin_us: ~3 x its expected time to a win, 2-50 ms; 2 ms beside CPU
+// workers): a serial client's reply then leaves as soon as the job is decided instead of after a condition-variable
+// wake-up (decided -> result in the client p50 11 -> 6 us), and a search far longer than
+// expected -- or one nobody expects to end -- is waited for asleep (round 6, ADVICE r05: a flat 50 ms before).
+// NANOPOW_WAIT_SPIN=0 turns it off (A/B runs).
 constexpr int kMaxSpinners = 2;
-constexpr int64_t kSpinUs = 2000;  // (round 6, ADVICE r05: was 50 ms, a whole send-difficulty search of one core each)
 std::atomic<int> g_spinners{0};
 const bool g_wait_spin = [] {
   const char* e = getenv("NANOPOW_WAIT_SPIN");
@@ -1812,8 +1841,9 @@ static int wait_job(const JobP& j, int64_t timeout_us, Done done, bool spin = fa
   const auto deadline = std::chrono::steady_clock::now() + std::chrono::microseconds(timeout_us < 0 ? 0 : timeout_us);
   if (spin && g_wait_spin && timeout_us != 0) {
     if (g_spinners.fetch_add(1, std::memory_order_relaxed) < kMaxSpinners) {
+      const int64_t spin_us = (int64_t)j->spin_us;
       const auto spin_end = std::chrono::steady_clock::now() +
-                            std::chrono::microseconds(timeout_us < 0 ? kSpinUs : std::min(timeout_us, kSpinUs));
+                            std::chrono::microseconds(timeout_us < 0 ? spin_us : std::min(timeout_us, spin_us));
       for (uint32_t k = 0; !done(); ++k) {
         cpu_relax();
         if ((k & 255u) == 0 && (std::chrono::steady_clock::now() >= spin_end ||

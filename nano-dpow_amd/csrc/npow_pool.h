@@ -67,6 +67,8 @@ struct Job {
   // the deciding one (CPU re-validation then decides at t_decide)
   double t_submit = 0, t_adopt = 0, t_launch = 0, t_win = 0, t_kend = 0, t_finish = 0, t_decide = 0, t_win_seen = 0;
   uint64_t gpu_t_win = 0;  // the deciding win's s_memrealtime (PoolWin::t; NANOPOW_TRACE_LATENCY GPU timelines)
+  double spin_us = 2000.0;  // how long its result waiters and the win watcher poll before they sleep (npow_pool.cpp
+                            // spin_window_us: ~3 x its expected time to a win, in [2, 50] ms)
 };
 using JobP = std::shared_ptr<Job>;
 

@@ -53,6 +53,7 @@ class Config:
     budget: bool = True                      # the launch's time budget may pass (hashing workgroups end)
     linger_timeout: bool = False             # lingering workgroups may reach their own budget and exit
     balance: bool = True                     # polls move a workgroup to a less crowded entry
+    entries: int = 2                         # successive dynamic entries (1 or 2; tuples above are indexed by entry)
     # seeded bugs (the checker's own test: each must be caught)
     bug_leave_own_shard: bool = False        # the last leaver checks only its own shard before publishing
     bug_join_no_recheck: bool = False        # a joiner hashes without checking the dead word after its count-up
@@ -67,9 +68,8 @@ Local = tuple  # (pc, e, local, stop, end, looked, over, tmp, k, attempt, nd_vie
 
 
 def initial(cfg: Config):
-    S = cfg.shards
-    shared = ((0,) * N_ENT, ((0,) * S,) * N_ENT, (0,) * N_ENT, (-1,) * N_ENT, (0,) * N_ENT, 0, 0, 0, 0, (0, 0), 0,
-              (False,) * N_ENT, (0,) * N_ENT)
+    S, N = cfg.shards, cfg.entries
+    shared = ((0,) * N, ((0,) * S,) * N, (0,) * N, (-1,) * N, (0,) * N, 0, 0, 0, 0, (0, 0), 0, (False,) * N, (0,) * N)
     # every workgroup of the launch starts lingering (an empty lingering launch, Worker::launch(true))
     locs = tuple(("LOOK", -1, 0, 0, 0, 0, 0, 0, 0, 0, 0, None) for _ in range(cfg.workgroups))
     return shared, locs
@@ -92,6 +92,7 @@ class Model:
     def host_moves(self, sh, locs) -> List[Tuple[str, Shared]]:
         cfg = self.cfg
         dead, wgs, done, fin, kill, kills, kd, nd, yld, mirror, budget, won, khost = sh
+        N_ENT = cfg.entries
         out = []
         if nd < N_ENT and not yld:
             # the next search's entry (dyn_add): the previous one must be decided first (a serial client)
@@ -382,6 +383,7 @@ def check(cfg: Config, max_states: int = 3_000_000, want_trace: bool = True, sto
             kinds.add(kind)
             violations.append((kind, trace(st) if want_trace else []))
 
+    N_ENT = cfg.entries
     while stack and not (stop_at_first and violations):
         st = stack.pop()
         sh, locs = st

@@ -24,6 +24,9 @@ CLEAN = {
     "win-both": pm.Config(kill=(False, False), win=(True, True)),
     "kill0-win1-no-relay": pm.Config(relay=False),
     "kill0-win1-linger-timeout": pm.Config(linger_timeout=True, budget=False),
+    # three workgroups, two on one shard, on one entry won here (the multi-leaver publish race)
+    "three-workgroups-win": pm.Config(workgroups=3, shard_of=(0, 0, 1), entries=1, kill=(False, False),
+                                      win=(True, False), budget=False),
 }
 
 
