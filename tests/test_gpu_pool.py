@@ -369,9 +369,10 @@ def test_wait_result_returns_at_the_decision(gpu_engine):
 
 def test_a_long_search_does_not_spin_a_core(gpu_engine):
     """the win watcher spun one core for as long as any slot was armed (a whole long search, an idle
-    lingering launch), and result waiters spun up to 50 ms per call.  Now it spins only for 2 ms after an arm or a
-    record it handled, and waiters for 2 ms: over a second of an endless search nobody waits on, the process uses a
-    fraction of a core (the pool worker's naps and the watcher's 20-us naps), not the one a spinning thread costs."""
+    lingering launch), and result waiters spun up to 50 ms per call.  Now both spin only within the job's spin window
+    (~3x its expected time to a win, at most 50 ms -- the cap for a search that cannot end): over a second of an endless
+    search nobody waits on, the process uses a fraction of a core (the pool worker's naps and the watcher's 20-us
+    naps), not the one a spinning thread costs."""
     tok = _lib.CancelToken()
     t = gpu_engine.submit(bytes(range(100, 132)), M64, device_mask=1, cancel=tok)
     try:
