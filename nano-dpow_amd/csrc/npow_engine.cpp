@@ -469,12 +469,16 @@ int npow_init(int* n_devices) try {
       std::lock_guard<std::mutex> g(g_mu);
       if (!g_init) return;
       if (!pool_exit()) return;
-      std::thread([] {
-        for (auto& d : g_devs) {
-          std::unique_lock<std::mutex> lk(d->mu, std::try_to_lock);
-          if (lk.owns_lock()) free_device(*d);
-        }
-      }).join();
+      try {
+        std::thread([] {
+          for (auto& d : g_devs) {
+            std::unique_lock<std::mutex> lk(d->mu, std::try_to_lock);
+            if (lk.owns_lock()) free_device(*d);
+          }
+        }).join();
+      } catch (...) {  // no thread to be had at exit: leave the devices to the runtime's teardown
+        return;
+      }
       g_init = false;
     });
   }

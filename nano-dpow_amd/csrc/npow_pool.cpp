@@ -696,12 +696,11 @@ class Worker {
   void handle_win(int s);
   bool win_published(int s) const;
   void early_finish(int s);
-  // A stale slot's final count came after all (late): how late on the GPU's clock, after the job's deciding win
-  // (npow_device_stats.stale_gpu_delay_us; one clock for CU partitions of one GPU)
-  void stale_fin_came(int s) {
-    const Slot& sl = slots_[s];
+  // A stale slot's final count came after all (late): how late on the GPU's clock, after the job's deciding win at tw
+  // (Job::gpu_t_win, read by the caller under g_pool.mu; npow_device_stats.stale_gpu_delay_us; one clock for CU
+  // partitions of one GPU)
+  void stale_fin_came(int s, uint64_t tw) {
     const uint64_t tf = __atomic_load_n(&d_.pmb->fin[s].t_fin, __ATOMIC_RELAXED);
-    const uint64_t tw = sl.job ? sl.job->gpu_t_win : 0;
     std::lock_guard<std::mutex> sg(d_.stats_mu);
     d_.stale_late++;
     if (tw && tf > tw) d_.stale_gpu_delay_us = std::max(d_.stale_gpu_delay_us, (double)(tf - tw) / 100.0);
@@ -1046,7 +1045,7 @@ void Worker::early_finish(int s) {
     std::lock_guard<std::mutex> sg(d_.stats_mu);
     d_.linger_relays++;
   }
-  if (sl.stale) stale_fin_came(s);
+  if (sl.stale) stale_fin_came(s, j.gpu_t_win);
   if (d_.dead || sl.requeue || !j.decided.load()) return;
   sl.early = true;
   const uint64_t delta = total - sl.baseline;
@@ -1394,7 +1393,12 @@ int Worker::retire() {
     if (win_published(s)) handle_win(s);  // published by the last launch, not yet seen
     if (sl.stale && !sl.fin_seen) {  // every launch that held it has ended: its count came late, or never
       if (__atomic_load_n(&d_.pmb->fin[s].gen, __ATOMIC_ACQUIRE) == sl.gen) {
-        stale_fin_came(s);
+        uint64_t tw = 0;
+        {
+          std::lock_guard<std::mutex> g(g_pool.mu);
+          tw = sl.job ? sl.job->gpu_t_win : 0;
+        }
+        stale_fin_came(s, tw);
       } else {
         std::lock_guard<std::mutex> sg(d_.stats_mu);
         d_.stale_missing++;
