@@ -150,8 +150,8 @@ def issue_bound_cycles(mix):
     full = mix["valu"] - adds - aligns
     return 4 * (adds + aligns + max(0, full - aligns) / 2)
 # rocprofv3 PMC passes of the bench's own command (tools/pmc_bench.sh), newest first
-PMC_POOL = ("r06g_pmc_pool.json", "r06f_pmc_pool.json", "r05av_pmc_pool.json", "r05au_pmc_pool.json", "r05am_pmc_pool.json", "r05ak_pmc_pool.json", "r05f_pmc_pool.json", "r04j_pmc_pool.json", "r04i_pmc_pool.json", "r04h_pmc_pool.json", "r04g_pmc_pool.json", "r04f_pmc_pool.json", "r04e_pmc_pool.json", "r03s_pmc_pool.json", "r03w_pmc_pool.json", "r03p_pmc_pool.json", "r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
-PMC_SWEEP = ("r06g_pmc_sweep.json", "r06f_pmc_sweep.json", "r05av_pmc_sweep.json", "r05au_pmc_sweep.json", "r05am_pmc_sweep.json", "r05ak_pmc_sweep.json", "r05f_pmc_sweep.json", "r04j_pmc_sweep.json", "r04i_pmc_sweep.json", "r04h_pmc_sweep.json", "r04g_pmc_sweep.json", "r04f_pmc_sweep.json", "r04e_pmc_sweep.json", "r03s_pmc_sweep.json", "r03w_pmc_sweep.json", "r03p_pmc_sweep.json", "r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
+PMC_POOL = ("r06q_pmc_pool.json", "r06g_pmc_pool.json", "r06f_pmc_pool.json", "r05av_pmc_pool.json", "r05au_pmc_pool.json", "r05am_pmc_pool.json", "r05ak_pmc_pool.json", "r05f_pmc_pool.json", "r04j_pmc_pool.json", "r04i_pmc_pool.json", "r04h_pmc_pool.json", "r04g_pmc_pool.json", "r04f_pmc_pool.json", "r04e_pmc_pool.json", "r03s_pmc_pool.json", "r03w_pmc_pool.json", "r03p_pmc_pool.json", "r03_pmc_pool.json", "r02_ls2_pmc_pool.json")
+PMC_SWEEP = ("r06q_pmc_sweep.json", "r06g_pmc_sweep.json", "r06f_pmc_sweep.json", "r05av_pmc_sweep.json", "r05au_pmc_sweep.json", "r05am_pmc_sweep.json", "r05ak_pmc_sweep.json", "r05f_pmc_sweep.json", "r04j_pmc_sweep.json", "r04i_pmc_sweep.json", "r04h_pmc_sweep.json", "r04g_pmc_sweep.json", "r04f_pmc_sweep.json", "r04e_pmc_sweep.json", "r03s_pmc_sweep.json", "r03w_pmc_sweep.json", "r03p_pmc_sweep.json", "r03_pmc_sweep.json", "r02_ls2_pmc_sweep.json")
 METRIC = "Gnonce/s blake2b-64 per GPU & 8-GPU node; p50 time-to-work at fffffff8"
 CSRC = os.path.join(HERE, "nano-dpow_amd", "csrc")
 
