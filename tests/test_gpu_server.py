@@ -56,6 +56,20 @@ def test_send_difficulty_generate_and_validate(gpu_server):
         assert chk["valid_all"] == "1" and chk["valid_receive"] == "1"
 
 
+def test_multiplier_requests_on_gpu(gpu_server):
+    """A work_generate by multiplier (nano-work-server.exe @1680488 "multiplier"; the rule of dpow_server.py:250-305,
+    restated in nanopow/work.py): the threshold derived from the base difficulty, the work re-validated under hashlib
+    at it, and the reply's difficulty / multiplier those of the work's own value (SURVEY.md §8 A6 on the GPU path)."""
+    from nanopow import work as W
+    for i, m in enumerate(["1.0", "2.5", "0.125"]):
+        h = f"{i + 100:064X}"
+        thr = W.from_multiplier(float(m), W.DEFAULT_BASE)
+        r = post(gpu_server.address, {"action": "work_generate", "hash": h, "multiplier": m})
+        v = oracle.work_value_hashlib(bytes.fromhex(h), int(r["work"], 16))
+        assert v >= thr and r["difficulty"] == f"{v:016x}", (m, r)
+        assert float(r["multiplier"]) == pytest.approx(W.to_multiplier(v, W.DEFAULT_BASE), rel=1e-9), (m, r)
+
+
 def test_benchmark_on_gpu(gpu_server):
     """`benchmark` (nano-work-server.exe @1679992..1680344): count searches of random roots at the
     base difficulty, timed end to end; fields and arithmetic as the reference reports them."""
