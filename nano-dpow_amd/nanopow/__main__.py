@@ -113,8 +113,21 @@ def build(args: argparse.Namespace):
     return srv
 
 
+def _stop_on_sigterm() -> None:
+    """SIGTERM (systemd's stop, `kill`) ends the server as Ctrl-C does: serve_forever is interrupted in the main thread,
+    the listener closes, and the process exits normally -- so libnanopow's exit hook drains the running searches and
+    frees the GPUs (round 6) instead of the process dying with launches in flight."""
+    import signal
+
+    def handler(signum, frame):
+        raise KeyboardInterrupt(f"signal {signum}")
+
+    signal.signal(signal.SIGTERM, handler)
+
+
 def main(argv=None) -> int:
     args = parse_args(argv)
+    _stop_on_sigterm()
     logging.basicConfig(level=logging.DEBUG if args.verbose else logging.INFO,
                         format="%(asctime)s %(levelname)s %(message)s")
     srv = build(args)

@@ -78,3 +78,57 @@ def test_regime_child_exits_cleanly(profiled):
     assert rec["stale_final_counts"]["missing"] == 0, rec["stale_final_counts"]  # no final count lost
     if profiled:
         assert traced, "rocprofv3 wrote no trace"
+
+
+def test_work_server_stops_on_sigterm_with_searches_running():
+    """`python -m nanopow` under systemd is stopped with SIGTERM: the server turns it into an orderly stop (the pending
+    work_generate requests answered {"error": "Cancelled"}, the listener closed) and a normal exit, so the library's exit
+    hook drains and frees the GPU -- rc 0, not death by signal with launches in flight."""
+    import json
+    import signal
+    import socket
+    import threading
+    import time
+    import urllib.request
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, PYTHONPATH=os.path.join(ROOT, "nano-dpow_amd"))
+    p = subprocess.Popen([sys.executable, "-m", "nanopow", "-l", f"127.0.0.1:{port}"], cwd=ROOT, env=env,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        deadline = time.time() + 90
+        ready = False
+        while time.time() < deadline and not ready:
+            line = p.stderr.readline()
+            if not line:
+                break
+            ready = "Ready to receive requests" in line
+        assert ready, "the work server did not come up"
+        replies = []
+
+        def generate(i):
+            body = json.dumps({"action": "work_generate", "hash": f"{i + 7:064x}", "difficulty": "ffffffffffffffff"})
+            req = urllib.request.Request(f"http://127.0.0.1:{port}", data=body.encode(), method="POST",
+                                         headers={"Content-Type": "application/json"})
+            try:
+                with urllib.request.urlopen(req, timeout=30) as r:
+                    replies.append(json.loads(r.read()))
+            except Exception as e:  # (a reply cut off by the exit would land here; recorded)
+                replies.append({"exception": repr(e)})
+
+        ths = [threading.Thread(target=generate, args=(i,), daemon=True) for i in range(2)]
+        for t in ths:
+            t.start()
+        time.sleep(0.5)  # both searches running (endless at this threshold)
+        p.send_signal(signal.SIGTERM)
+        rc = p.wait(30)
+        for t in ths:
+            t.join(10)
+    finally:
+        if p.poll() is None:
+            p.kill()
+            p.wait(10)
+    assert rc == 0, (rc, p.stderr.read()[-3000:])
+    assert replies and all(r == {"error": "Cancelled"} for r in replies), replies

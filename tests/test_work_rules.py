@@ -136,3 +136,20 @@ def test_gpu_threads_is_a_lower_bound_on_the_launch():
     assert apply_threads(e, [(0, 0, (1 << 32) + 1)]) == 16386
     assert apply_threads(e, [(0, 0, 1 << 31)]) == 0                       # exactly the default launch
     assert apply_threads(e, [(0, 0, 1 << 40)]) == 65536                   # capped
+
+
+def test_sigterm_stops_the_server_like_ctrl_c():
+    """`python -m nanopow` turns SIGTERM into the KeyboardInterrupt that ends serve_forever, so a stopped server exits
+    normally and libnanopow's exit hook drains and frees the GPUs (tests/test_gpu_exit.py checks it on the GPU)."""
+    import os
+    import signal
+    import time
+    from nanopow.__main__ import _stop_on_sigterm
+    old = signal.getsignal(signal.SIGTERM)
+    try:
+        _stop_on_sigterm()
+        with pytest.raises(KeyboardInterrupt):
+            os.kill(os.getpid(), signal.SIGTERM)
+            time.sleep(2)
+    finally:
+        signal.signal(signal.SIGTERM, old)
