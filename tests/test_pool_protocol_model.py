@@ -8,7 +8,7 @@ killed by another device's win, with the launch's budget passing at any point.  
 Asserted: no final count is ever published short (EXACT) and no won or killed entry of a still-lingering launch is
 left without one (FIN) -- with and without round 6's lingering relay -- and, so that a clean result means something,
 each of three seeded bugs is caught.  Round 5's rare unpublished count is not a hole of this logic: the model finds
-none.  On the GPU, since round 6's lingering relay and the stale classification, no count has been stale in 11,400 searches
+none.  On the GPU, since round 6's lingering relay and the stale classification, no count has been stale in over 20,000 searches
 over 4 and 8 partitions; should one be, the worker tells late from missing (npow_device_stats.stale_late /
 stale_missing; DESIGN.md sections 1 and 4).
 """
