@@ -139,6 +139,25 @@ def test_value_range_2p28_shipped_stream(gpu_engine):
             assert bad.size == 0, f"root {root_hex[:8]}: {bad.size} values differ from {s + int(bad[0]):#x} on"
 
 
+def test_value_range_2p32_shipped_stream(gpu_engine):
+    """2^32 consecutive full 64-bit values of the shipped stream -- a whole 32-bit nonce span, across the carry into bit
+    32 -- every one equal to the oracle's (north_star: "identical 64-bit work values for any nonce"): 256 launches of
+    2^24, each compared in full with the C oracle on the box's CPUs (16 threads).  Also a checksum: the values' sum
+    mod 2^64 over the whole span, GPU against oracle."""
+    root = bytes.fromhex("3B7F1E0C9A2D4F6B8C1E3A5D7F9B0C2E4A6D8F1B3C5E7A9D0F2B4C6E8A1D3F5B")
+    start = (1 << 31) * 3  # [3 * 2^31, 5 * 2^31): bit 32 carries at 2^32 (a quarter in) and bit 33 at 2^33
+    total_gpu = total_cpu = 0
+    for k in range(256):
+        s = start + (k << 24)
+        got = gpu_engine.values_array(root, s, 1 << 24, path=_lib.NPOW_PATH_SEARCH)
+        want = oracle.work_values_range(root, s, 1 << 24)
+        bad = np.flatnonzero(got != want)
+        assert bad.size == 0, f"{bad.size} values differ from {s + int(bad[0]):#x} on"
+        total_gpu = (total_gpu + int(got.sum(dtype=np.uint64))) & ((1 << 64) - 1)
+        total_cpu = (total_cpu + int(want.sum(dtype=np.uint64))) & ((1 << 64) - 1)
+    assert total_gpu == total_cpu
+
+
 def test_sweep_fixtures(gpu_engine):
     for c in load_golden("sweeps_small.json")["cases"]:
         got = gpu_engine.sweep(bytes.fromhex(c["root"]), int(c["threshold"], 16), int(c["start"], 16), c["count"])
