@@ -4,7 +4,7 @@ Bit-exact throughout (integer work).  Run on an MI355X: ``pytest -m gpu``.
 Covers: every golden (root, nonce, value) triple through all three GPU hash paths
 (npow_values = the stream the search and sweep kernels run, the seq stream, the generic
 per-lane-root kernel); contiguous value ranges incl. 2^32 and 2^64 carries and 2^20 / 2^24
-ranges, and 2^28 consecutive values of the shipped stream for two roots; every exhaustive sweep
+ranges, 2^28 consecutive values of the shipped stream for two roots and 2^32 for a third; every exhaustive sweep
 fixture (8 roots x [0, 2^28), hashlib ranges, the range across 2^64 -> 0) and,
 at BASELINE config 3's full size, the 2^36 sweep; first-win search validity
 at the BASELINE thresholds; threshold edges; exhaustion, cancellation,
